@@ -1,0 +1,16 @@
+"""Shared pytest configuration: the `gpu` marker and import paths.
+
+`-m "not gpu"` runs the oracle-vs-golden, host-logic and ABI-load tests on CPU;
+`-m gpu` runs the HIP parity tests (through the C-ABI) on an MI355X.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through libpifft.so)")
