@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""bench.py -- the headline benchmark of BASELINE.json:
+
+  "GFLOP/s (5N log2N / t) + % HBM roofline, fp64 complex N=2^28 @1/2/4/8 GPU"
+
+One step = one complete pi-FFT of ONE fp64 complex N=2^28 transform (config 4
+at --gpus 1).  With --gpus G (one process per GPU, torchrun) the same transform
+is split over P=G workers the reference's way: rank q computes worker q's
+N/P output bins (its tree over the whole, replicated input + an N/P-point FFT),
+with no data-path collective; the time is the slowest rank's (max over ranks),
+value = 5 N log2 N / t for the one transform ("strong" scaling: the total work
+is fixed).  Inputs are generated on the device (splitmix64, the oracle's
+generator) and resident in HBM before the timed region.
+
+Adds to the JSON line:
+  roofline     : the dominant kernel's algorithmic bytes / its mean duration
+                 (HIP events on the launch stream, inside the timed region),
+                 vs 8 TB/s; traffic = PMC-measured HBM bytes per launch from the
+                 committed rocprofv3 summary (profiles/), else null
+  cpu_baseline : the reference CPU path (oracle/_ref, compiled from the
+                 reference source) on a bounded sample, rank 0 at --gpus 1 only
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import re
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def _baseline_metric():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        return json.load(f)["metric"]
+
+
+def cpu_baseline(log_n: int, threads: int) -> dict | None:
+    """Reference CPU path (oracle/_ref, -Dfloat=double) on N=2^log_n with P=threads."""
+    import pifft_oracle as oracle
+    n = 1 << log_n
+    flops = 5.0 * n * log_n
+    exe = oracle.reference_binary(64)
+    if exe:
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, "-n", str(n), "-p", str(threads), "-o"], capture_output=True, text=True,
+                           timeout=900)
+        wall = time.perf_counter() - t0
+        if r.returncode == 0:
+            cols = r.stdout.strip().splitlines()[-1].split("\t")
+            ms = float(cols[2])
+            return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
+                    "kind": "reference",
+                    "sample": f"reference fourier-parallel-pi-cpu-pthreads built -O2 -Dfloat=double, "
+                              f"fp64 N=2^{log_n}, p={threads} pthreads; worker 0's tree+cylinder time "
+                              f"{ms:.1f} ms (the reference's own timer); process wall {wall:.1f} s"}
+    # fallback: the C restatement (bitwise-equal arithmetic)
+    import numpy as np
+    x = oracle.generate(n, np.complex128)
+    _, (t1, t2, wall) = oracle.fft(x, P=threads, nthreads=threads, timing=True)
+    ms = t1 + t2
+    return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/pifft_oracle.c (restated reference) fp64 N=2^{log_n}, {threads} threads; "
+                      f"worker 0 tree+cylinder {ms:.1f} ms, join wall {wall:.1f} ms"}
+
+
+def load_traffic(config_key: str, launch_index: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("config_key") == config_key:
+            per = d.get("per_launch_bytes", {})
+            v = per.get(str(launch_index))
+            if v is not None:
+                return float(v), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=28)
+    ap.add_argument("--prec", type=int, default=64, choices=(32, 64))
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=0, help="P (default: number of ranks)")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--allgather", action="store_true", help="also time the optional RCCL all-gather")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-log-n", type=int, default=26)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import pifft
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier(device_ids=[local])
+
+    n = 1 << args.log_n
+    P = args.workers or world
+    import pifft_dist
+    first, count = pifft_dist.worker_range(rank, world, P)
+    prec = pifft.F64 if args.prec == 64 else pifft.F32
+    cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
+    esz = 16 if prec == pifft.F64 else 8
+
+    if count == P:
+        plan = pifft.Plan(n, P, args.batch, prec, first=0, count=P, device=local, flags=pifft.OUT_NATURAL)
+    else:
+        plan = pifft.Plan(n, P, args.batch, prec, first=first, count=count, device=local,
+                          flags=pifft.OUT_SLICES)
+    desc = plan.describe()
+    stream = torch.cuda.current_stream(dev)
+    x = torch.empty(n * args.batch, dtype=cdt, device=dev)
+    pifft.generate_device(x.data_ptr(), n * args.batch, n, prec, seed=args.seed, stream=stream)
+    y = torch.empty(desc["out_elems"], dtype=cdt, device=dev)
+    for _ in range(args.warmup):
+        plan.execute_device(x.data_ptr(), y.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+
+    nl = desc["num_launches"]
+    sums = [0.0] * nl
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ms = plan.execute_device_timed(x.data_ptr(), y.data_ptr(), stream)
+        for i, m in enumerate(ms):
+            sums[i] += m
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = pifft_dist.max_over_ranks(elapsed, dev)
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    allgather_ms = None
+    if args.allgather and dist is not None and count < P:
+        torch.cuda.synchronize(dev)
+        barrier()
+        ta = time.perf_counter()
+        gathered = pifft_dist.allgather_slices(y)
+        natural = torch.empty(n * args.batch, dtype=cdt, device=dev)
+        pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), n, P, args.batch, prec, stream)
+        torch.cuda.synchronize(dev)
+        allgather_ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, dev)
+        del gathered, natural
+
+    avg = [s / args.steps for s in sums]
+    dom = max(range(nl), key=lambda i: avg[i]) if nl else 0
+    dom_bytes = desc["launch_bytes"][dom] if dom < len(desc["launch_bytes"]) else 0
+    achieved = dom_bytes / (avg[dom] * 1e-3) / 1e9 if avg and avg[dom] > 0 else 0.0
+    flops = 5.0 * n * args.log_n * args.batch
+    value = flops / (ms_per_step * 1e-3) / 1e9
+    config_key = f"n2^{args.log_n}_f{args.prec}_b{args.batch}_P{P}_q{count}"
+    traffic, traffic_src = load_traffic(config_key, dom)
+
+    launches = []
+    for i in range(nl):
+        kind = desc["launch_kind"][i] if i < len(desc["launch_kind"]) else "?"
+        b = desc["launch_bytes"][i] if i < len(desc["launch_bytes"]) else 0
+        launches.append({"kind": kind, "ms": round(avg[i], 4),
+                         "GB/s": round(b / (avg[i] * 1e-3) / 1e9, 1) if avg[i] > 0 else None})
+    total_bytes = sum(desc["launch_bytes"][:nl])
+
+    if rank == 0:
+        line = {
+            "metric": _baseline_metric(),
+            "value": round(value, 2),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64" if prec == pifft.F64 else "f32",
+            "data": "synthetic: splitmix64 U[-1,1]/sqrt(N) complex input generated in HBM (the oracle's generator)",
+            "config": {
+                "workload": (f"config 4: one fp64 complex N=2^{args.log_n} pi-FFT" if args.log_n == 28 and
+                             args.prec == 64 and args.batch == 1 else
+                             f"pi-FFT N=2^{args.log_n} f{args.prec} batch {args.batch}")
+                            + f", P={P} workers, {count} per GPU (no data-path collective)",
+                "n": n, "workers": P, "workers_per_gpu": count, "batch": args.batch,
+                "local_n": desc["local_n"], "passes": desc["num_passes"], "radix": desc["radix"],
+                "lines_per_workgroup": desc["lines"],
+                "hbm_bytes_per_step_algorithmic": total_bytes,
+                "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                "launches": launches,
+                "parallelism": f"pi-split p{P} over {world} GPU(s)",
+                "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"launch {dom} ({launches[dom]['kind'] if launches else '?'})",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes": dom_bytes,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads
+            ncpu = os.cpu_count() or 1
+            while threads > ncpu:
+                threads //= 2
+            try:
+                line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, max(1, threads))
+            except Exception as e:  # reported, never silently replaced
+                line["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

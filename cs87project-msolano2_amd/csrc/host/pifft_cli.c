@@ -1,0 +1,379 @@
+/*
+ * pifft_cli.c -- C host of the MI355X pi-FFT: the reference's command line
+ * and output contract, with the transform running on GPUs through the
+ * C-ABI of libpifft.so (include/pifft.h).
+ *
+ * Mirrors benchmark/fourier/parallel/pi/cpu/pthreads/fourier-parallel-pi-cpu-pthreads.c
+ * (CPU.c):   main            CPU.c:98-113
+ *            setup_from_args CPU.c:125-211   same flags, same messages
+ *            initialize_data CPU.c:220-275   (synthetic input, or the -t vector)
+ *            run             CPU.c:312-380   (workers -> GPUs instead of pthreads)
+ *            show_usage, print_input/print_output, verify_results (CPU.c:293-302, 659-705)
+ *
+ *   pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b batch] [-s seed] [-g gpus]
+ *         [-w file] [-x] [-W warmups] [-l]
+ *
+ * Output: the reference's 5-column TSV "n p total stage1 stage2" in ms
+ * (CPU.c:485-492), once.  stage 1 = tree, stage 2 = local FFT (+ reorder).
+ * With several GPUs the time is the slowest GPU's (the reference prints worker
+ * 0's own timers without a barrier; here all GPUs are waited for).
+ * Extensions: -f precision (default 32 = the reference's data_t), -b batch of
+ * independent transforms, -s seed (default: hash of the time, as CPU.c:244),
+ * -g number of GPUs the P workers are spread over (default 1), -w dump the
+ * natural-order output (binary), -x extra columns (GFLOP/s, GB/s),
+ * -W untimed warm-up runs before the timed one (default 1; code-object load),
+ * -l list GPUs (the how-many-* utilities).  -n is parsed as 64-bit.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "pifft.h"
+
+#define stderr_out(...) fprintf(stderr, __VA_ARGS__), fflush(stderr)
+#define print_out(...) printf(__VA_ARGS__), fflush(stdout)
+
+typedef struct tr {
+    uint64_t N;          /* input size                         (CPU.c:41) */
+    uint32_t P;          /* number of workers                  (CPU.c:42) */
+    void* in;            /* input                              (CPU.c:44) */
+    void* out;           /* output, natural order              (CPU.c:45) */
+    uint32_t test_mode;  /* -t                                 (CPU.c:48) */
+    uint32_t no_header;  /* -o                                 (CPU.c:49) */
+    int prec;            /* -f: 32 or 64 */
+    uint32_t batch;      /* -b */
+    uint64_t seed;       /* -s */
+    int seed_given;
+    uint32_t gpus;       /* -g */
+    const char* dump;    /* -w */
+    int extra;           /* -x */
+    int warmups;         /* -W */
+} tr_t;
+
+static void show_usage(void) {
+    print_out("\nusage:\n"
+              "  pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b <batch>] [-s <seed>]\n"
+              "        [-g <gpus>] [-w <file>] [-x] [-W <warmups>] [-l]\n"
+              "\noptions:\n"
+              "  -n <n>     power of two input size\n"
+              "  -p <p>     power of two number of processors (less than n)\n"
+              "  -o         omit timing headers\n"
+              "  -t         compare against precomputed input/output\n"
+              "  -f 32|64   precision (default 32, the reference's data_t)\n"
+              "  -b <b>     batch of independent transforms (default 1)\n"
+              "  -s <seed>  input seed (default: hash of the time)\n"
+              "  -g <g>     GPUs to spread the p workers over (default 1)\n"
+              "  -w <file>  write the natural-order output (binary data_t)\n"
+              "  -x         extra columns: GFLOP/s, algorithmic GB/s\n"
+              "  -W <w>     untimed warm-up runs (default 1)\n"
+              "  -l         list GPUs and exit\n"
+              "\n");
+}
+
+static int is_power_of_two_u64(uint64_t x) { return x && !(x & (x - 1)); }
+
+/* CPU.c:769-774 (Wang hash), used to seed from the time like CPU.c:244 */
+static uint32_t hash(uint32_t x) {
+    x = (x + 0x7ed55d16U) + (x << 12);
+    x = (x ^ 0xc761c23cU) ^ (x >> 19);
+    x = (x + 0x165667b1U) + (x << 5);
+    x = (x + 0xd3a2646cU) ^ (x << 9);
+    x = (x + 0xfd7046c5U) + (x << 3);
+    x = (x ^ 0xb55a4f09U) ^ (x >> 16);
+    return x;
+}
+
+static int parse_u64(const char* s, uint64_t* v) {
+    char* end = NULL;
+    if (!s || !*s) return -1;
+    unsigned long long x = strtoull(s, &end, 10);
+    if (*end) return -1;
+    *v = (uint64_t)x;
+    return 0;
+}
+
+/* CPU.c:125-211: later options override earlier ones (so "-t -n 16" keeps the
+ * test vector but transforms 16 points, as in the reference). */
+int setup_from_args(tr_t* t, int argc, char** argv) {
+    int ret;
+    uint64_t num = 0;
+    memset(t, 0, sizeof(tr_t));
+    t->prec = PIFFT_F32;
+    t->batch = 1;
+    t->gpus = 1;
+    t->warmups = 1;
+    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:xW:l")) != -1) {
+        switch (ret) {
+            case 'n':
+                if (parse_u64(optarg, &num) || !(num > 1) || !is_power_of_two_u64(num)) {
+                    stderr_out("Invalid input size (should be 2^i for i>0)\n");
+                    show_usage();
+                    goto err;
+                }
+                t->N = num;
+                break;
+            case 'p':
+                if (parse_u64(optarg, &num) || !(num > 0) || !is_power_of_two_u64(num) || num > 0x80000000ULL) {
+                    stderr_out("Invalid number of procs (should be 2^i for i>0)\n");
+                    show_usage();
+                    goto err;
+                }
+                t->P = (uint32_t)num;
+                break;
+            case 'o':
+                t->no_header = 1;
+                break;
+            case 't':
+                print_out("Test mode (ignoring provided input size, if any)...\n");
+                t->N = 8;
+                t->test_mode = 1;
+                break;
+            case 'f':
+                if (strcmp(optarg, "32") && strcmp(optarg, "64")) {
+                    stderr_out("Invalid precision (should be 32 or 64)\n");
+                    show_usage();
+                    goto err;
+                }
+                t->prec = atoi(optarg);
+                break;
+            case 'b':
+                if (parse_u64(optarg, &num) || num < 1 || num > 0xFFFFFFFFULL) {
+                    stderr_out("Invalid batch (should be >= 1)\n");
+                    goto err;
+                }
+                t->batch = (uint32_t)num;
+                break;
+            case 's':
+                if (parse_u64(optarg, &num)) {
+                    stderr_out("Invalid seed\n");
+                    goto err;
+                }
+                t->seed = num;
+                t->seed_given = 1;
+                break;
+            case 'g':
+                if (parse_u64(optarg, &num) || !(num > 0) || !is_power_of_two_u64(num) || num > 1024) {
+                    stderr_out("Invalid number of GPUs (should be 2^i)\n");
+                    goto err;
+                }
+                t->gpus = (uint32_t)num;
+                break;
+            case 'w':
+                t->dump = optarg;
+                break;
+            case 'x':
+                t->extra = 1;
+                break;
+            case 'W':
+                if (parse_u64(optarg, &num) || num > 1000) {
+                    stderr_out("Invalid warm-up count\n");
+                    goto err;
+                }
+                t->warmups = (int)num;
+                break;
+            case 'l': {
+                int n = pifft_gpu_count();
+                if (n < 0) {
+                    stderr_out("%s\n", pifft_last_error());
+                    goto err;
+                }
+                print_out("%d\n", n);
+                exit(EXIT_SUCCESS);
+            }
+            case '?':
+                stderr_out("Unknown or missing arg %c\n", optopt);
+                show_usage();
+                goto err;
+        }
+    }
+    if (!t->N) {
+        stderr_out("Missing option: -n\n");
+        show_usage();
+        goto err;
+    }
+    if (!t->P) {
+        stderr_out("Missing option: -p\n");
+        show_usage();
+        goto err;
+    }
+    if (t->P > t->N) {
+        stderr_out("More processors than inputs!\n");
+        show_usage();
+        goto err;
+    }
+    {
+        int ngpu = pifft_gpu_count();
+        if (ngpu < 1) {
+            stderr_out("No GPU available (%s)\n", pifft_last_error());
+            goto err;
+        }
+        if (t->gpus > (uint32_t)ngpu) {
+            stderr_out("Too many GPUs! (only %d GPUs available)\n", ngpu);
+            goto err;
+        }
+        if (t->gpus > t->P) t->gpus = t->P; /* at least one worker per GPU */
+    }
+    return 0;
+err:
+    stderr_out("Could not setup the transform from the cmdline args\n");
+    return -1;
+}
+
+static size_t esz(const tr_t* t) { return t->prec == PIFFT_F64 ? 16 : 8; }
+
+static double re_at(const tr_t* t, const void* a, uint64_t i) {
+    return t->prec == PIFFT_F64 ? ((const double*)a)[2 * i] : ((const float*)a)[2 * i];
+}
+static double im_at(const tr_t* t, const void* a, uint64_t i) {
+    return t->prec == PIFFT_F64 ? ((const double*)a)[2 * i + 1] : ((const float*)a)[2 * i + 1];
+}
+static void set_at(const tr_t* t, void* a, uint64_t i, double re, double im) {
+    if (t->prec == PIFFT_F64) {
+        ((double*)a)[2 * i] = re;
+        ((double*)a)[2 * i + 1] = im;
+    } else {
+        ((float*)a)[2 * i] = (float)re;
+        ((float*)a)[2 * i + 1] = (float)im;
+    }
+}
+
+/* splitmix64 -> (2u-1)/sqrt(N): the same bytes as pifft_generate_device */
+static uint64_t splitmix64(uint64_t seed, uint64_t draw) {
+    uint64_t z = seed + (draw + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static void print_input(const tr_t* t) {
+    print_out("Input:\n");
+    for (uint64_t b = 0; b < t->N; b++) print_out("%.1f+%.1fi, ", re_at(t, t->in, b), im_at(t, t->in, b));
+    print_out("\n");
+}
+
+static void print_output(const tr_t* t) {
+    print_out("Output:\n");
+    for (uint64_t b = 0; b < t->N; b++) print_out("%.1f+%.1fi, ", re_at(t, t->out, b), im_at(t, t->out, b));
+    print_out("\n");
+}
+
+/* CPU.c:689-705 */
+static void verify_results(const tr_t* t) {
+    static const double want[8] = {4, 0, 0, 0, -4, 0, 0, 0};
+    int ok = t->N >= 8;
+    for (int i = 0; ok && i < 8; i++) ok = re_at(t, t->out, i) == want[i] && im_at(t, t->out, i) == 0.0;
+    print_out(ok ? "Output is correct. Test passed.\n\n" : "Output is incorrect! Test failed.\n\n");
+}
+
+/* CPU.c:220-275 */
+static int initialize_data(tr_t* t) {
+    const uint64_t total = t->N * (uint64_t)t->batch;
+    t->in = calloc(total, esz(t));
+    t->out = calloc(total, esz(t));
+    if (!t->in || !t->out) {
+        perror("malloc error");
+        stderr_out("Could not initialize the data\n");
+        return -1;
+    }
+    if (!t->test_mode) {
+        uint64_t seed = t->seed_given ? t->seed : (uint64_t)hash((uint32_t)time(NULL));
+        const double scale = sqrt((double)t->N);
+        for (uint64_t e = 0; e < total; e++) {
+            double ur = (double)(splitmix64(seed, 2 * e) >> 11) * 0x1.0p-53;
+            double ui = (double)(splitmix64(seed, 2 * e + 1) >> 11) * 0x1.0p-53;
+            set_at(t, t->in, e, (2.0 * ur - 1.0) / scale, (2.0 * ui - 1.0) / scale);
+        }
+    } else {
+        /* 0,1,0,1,0,1,0,1 (CPU.c:251-260) in every transform of the batch */
+        for (uint32_t b = 0; b < t->batch; b++)
+            for (uint64_t i = 0; i < 8 && i < t->N; i++) set_at(t, t->in, b * t->N + i, (double)(i & 1), 0.0);
+        print_input(t);
+    }
+    return 0;
+}
+
+static void cleanup_data(tr_t* t) {
+    free(t->in);
+    free(t->out);
+    t->in = t->out = NULL;
+}
+
+/* CPU.c:312-380: the P workers go to t->gpus GPUs, P/gpus consecutive workers
+ * each, and run concurrently; no data moves between GPUs. */
+int run(tr_t* t) {
+    pifft_plan* plans[1024] = {0};
+    const uint32_t G = t->gpus;
+    const uint32_t per = t->P / G;
+    int rc = -1;
+    double s1 = 0, s2 = 0;
+    if (initialize_data(t)) goto done;
+    for (uint32_t g = 0; g < G; g++) {
+        int r = (G == 1) ? pifft_plan_create_slices(&plans[g], t->N, t->P, 0, t->P, t->batch, t->prec, 0,
+                                                    PIFFT_OUT_NATURAL)
+                         : pifft_plan_create_slices(&plans[g], t->N, t->P, g * per, per, t->batch, t->prec,
+                                                    (int)g, PIFFT_OUT_SLICES);
+        if (r) {
+            stderr_out("(GPU %u): %s\n", g, pifft_last_error());
+            goto done;
+        }
+    }
+    for (int w = 0; w < t->warmups; w++) {
+        if (pifft_execute_group(plans, (int)G, t->in, NULL, NULL, NULL)) {
+            stderr_out("%s\n", pifft_last_error());
+            goto done;
+        }
+    }
+    if (pifft_execute_group(plans, (int)G, t->in, t->out, &s1, &s2)) {
+        stderr_out("%s\n", pifft_last_error());
+        goto done;
+    }
+    if (!t->test_mode) {
+        if (!t->no_header) print_out("n\tp\ttime (total)\ttime (stage 1)\ttime (stage 2)%s\n",
+                                     t->extra ? "\tGFLOP/s\tGB/s" : "");
+        if (t->extra) {
+            pifft_plan_info info;
+            uint64_t bytes = 0;
+            for (uint32_t g = 0; g < G; g++) {
+                pifft_plan_get_info(plans[g], &info);
+                for (int i = 0; i < info.num_launches && i < 64; i++) bytes += info.launch_bytes[i];
+            }
+            const double ms = s1 + s2;
+            const double flops = 5.0 * (double)t->N * log2((double)t->N) * t->batch;
+            print_out("%llu\t%u\t%lf\t%lf\t%lf\t%lf\t%lf\n", (unsigned long long)t->N, t->P, ms, s1, s2,
+                      flops / (ms * 1e6), (double)bytes / G / (ms * 1e6));
+        } else {
+            print_out("%llu\t%u\t%lf\t%lf\t%lf\n", (unsigned long long)t->N, t->P, s1 + s2, s1, s2);
+        }
+    } else {
+        print_output(t);
+        verify_results(t);
+    }
+    if (t->dump) {
+        FILE* f = fopen(t->dump, "wb");
+        if (!f || fwrite(t->out, esz(t), t->N * (uint64_t)t->batch, f) != t->N * (uint64_t)t->batch) {
+            perror("output dump");
+            if (f) fclose(f);
+            goto done;
+        }
+        fclose(f);
+    }
+    rc = 0;
+done:
+    for (uint32_t g = 0; g < G; g++)
+        if (plans[g]) pifft_plan_destroy(plans[g]);
+    cleanup_data(t);
+    if (rc) stderr_out("Could not run the transform\n");
+    return rc;
+}
+
+int main(int argc, char** argv) {
+    tr_t t;
+    if (setup_from_args(&t, argc, argv)) exit(EXIT_FAILURE);
+    if (run(&t)) exit(EXIT_FAILURE);
+    exit(EXIT_SUCCESS);
+}

@@ -1,0 +1,808 @@
+// cs87project-msolano2_amd/csrc/pifft.hip -- libpifft.so: planner + C-ABI shim.
+//
+// Implements include/pifft.h.  The host side plans the reference's two stages
+// (CPU.c:419-448 tree, CPU.c:463-478 cylinder) as a short list of kernel
+// launches (pifft_kernels.h) over device buffers:
+//
+//   tree    : input (batch x N, HBM-resident)  -> Z (batch x count x N/P)
+//   passes  : Z -> ... -> Z'   Stockham passes of the N/P-point local FFT,
+//             each an LDS-resident R-point sub-FFT over C adjacent lines
+//   [interleave: slice-major -> natural order, whole transform on one GPU]
+//
+// Buffers ping-pong between the caller's output and one plan-owned workspace.
+// Twiddles are host-built tables in HBM (w_R per pass, two-level w_M and w_N;
+// the tree uses the reference's own omega(N,k) formula up to N = 2^22 so that
+// its output is bit-identical to the reference's post-tree segment).
+#include "pifft_kernels.h"
+#include "../../include/pifft.h"
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+using namespace pifft;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return fail("%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+int env_int(const char* name, int dflt) {
+    const char* s = getenv(name);
+    return (s && *s) ? atoi(s) : dflt;
+}
+
+bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+int ilog2u(uint64_t x) {
+    int l = 0;
+    while (x > 1) { x >>= 1; l++; }
+    return l;
+}
+uint32_t bitrev(uint32_t x, int m) { return m ? (__builtin_bitreverse32(x) >> (32 - m)) : 0u; }
+
+// ---------------------------------------------------------------------------
+// pass kernel instantiations
+// ---------------------------------------------------------------------------
+struct PassKernel {
+    int prec, R, C;
+    const void* fn;
+    int nt;
+    int lds_bytes;
+};
+
+#define PK(T, PREC, R, C)                                                       \
+    PassKernel {                                                                \
+        PREC, R, C, reinterpret_cast<const void*>(&k_pass<T, R, C>),            \
+            PassCfg<R, C>::NT, PassCfg<R, C>::lds_elems * (int)sizeof(cx<T>)    \
+    }
+#define PK_C5(T, PREC, R) PK(T, PREC, R, 1), PK(T, PREC, R, 2), PK(T, PREC, R, 4), PK(T, PREC, R, 8), PK(T, PREC, R, 16)
+#define PK_C4(T, PREC, R) PK(T, PREC, R, 1), PK(T, PREC, R, 2), PK(T, PREC, R, 4), PK(T, PREC, R, 8)
+
+const PassKernel g_pass_kernels[] = {
+    // fp64 (16 B / element): LDS <= 160 KiB, <= 1024 threads
+    PK(double, 64, 2, 64), PK(double, 64, 4, 64), PK(double, 64, 8, 64),
+    PK_C5(double, 64, 16), PK_C5(double, 64, 32), PK_C5(double, 64, 64), PK_C5(double, 64, 128),
+    PK_C5(double, 64, 256), PK_C5(double, 64, 512), PK_C4(double, 64, 1024),
+    PK(double, 64, 2048, 1), PK(double, 64, 2048, 2), PK(double, 64, 2048, 4),
+    PK(double, 64, 4096, 1), PK(double, 64, 4096, 2), PK(double, 64, 8192, 1),
+    // fp32 (8 B / element)
+    PK(float, 32, 2, 64), PK(float, 32, 4, 64), PK(float, 32, 8, 64),
+    PK_C5(float, 32, 16), PK_C5(float, 32, 32), PK_C5(float, 32, 64), PK_C5(float, 32, 128),
+    PK_C5(float, 32, 256), PK_C5(float, 32, 512), PK_C5(float, 32, 1024), PK_C4(float, 32, 2048),
+    PK(float, 32, 4096, 1), PK(float, 32, 4096, 2), PK(float, 32, 4096, 4),
+    PK(float, 32, 8192, 1), PK(float, 32, 8192, 2), PK(float, 32, 16384, 1),
+};
+
+const PassKernel* find_pass(int prec, int R, int C) {
+    for (const auto& k : g_pass_kernels)
+        if (k.prec == prec && k.R == R && k.C == C) return &k;
+    return nullptr;
+}
+
+int max_lines(int prec, int R) {
+    int best = 0;
+    for (const auto& k : g_pass_kernels)
+        if (k.prec == prec && k.R == R && k.C > best) best = k.C;
+    return best;
+}
+
+// ---------------------------------------------------------------------------
+// plan
+// ---------------------------------------------------------------------------
+enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3 };
+enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, NBUF = 5 };
+
+struct Step {
+    int kind = 0;
+    const void* fn = nullptr;
+    dim3 grid, block;
+    size_t lds = 0;
+    int src = BUF_IN, dst = BUF_OUT;
+    uint64_t src_off = 0, dst_off = 0;  // elements
+    PassArgs pa{};
+    TreeArgs ta{};
+    TreeStageArgs tsa{};
+    int tree_kind = 0;  // 1 fused network, 2 staged level
+    uint64_t il_total = 0;
+    uint32_t il_log_n = 0, il_log_p = 0;
+    uint64_t bytes = 0;
+};
+
+}  // namespace
+
+struct pifft_plan {
+    uint64_t n = 0, m = 0;
+    uint32_t P = 1, q0 = 0, nq = 1, batch = 1;
+    int prec = 64, device = 0, flags = 0;
+    int lp = 0, log_n = 0, log_m = 0;
+    size_t esz = 16;
+    bool natural = true;
+    std::vector<Step> steps;
+    int tree_steps = 0, npasses = 0;
+    int radix[8] = {0}, lines[8] = {0};
+    void* buf[NBUF] = {nullptr};
+    size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0;
+    void* d_tw = nullptr;
+    size_t tw_bytes = 0;
+    hipStream_t stream = nullptr;
+    std::vector<hipEvent_t> ev;
+    void* d_hin = nullptr;   // pifft_execute's staging copies
+    void* d_hout = nullptr;
+    std::vector<char> host_tmp;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Host twiddle tables, appended to one blob (offsets 256-B aligned).
+struct TableBuilder {
+    std::vector<char> blob;
+    size_t esz;
+    explicit TableBuilder(size_t e) : esz(e) {}
+    size_t align() {
+        size_t off = (blob.size() + 255) & ~(size_t)255;
+        blob.resize(off);
+        return off;
+    }
+    void put(double re, double im) {
+        size_t o = blob.size();
+        blob.resize(o + esz);
+        if (esz == 16) {
+            double v[2] = {re, im};
+            memcpy(&blob[o], v, 16);
+        } else {
+            float v[2] = {(float)re, (float)im};
+            memcpy(&blob[o], v, 8);
+        }
+    }
+    // w_L^(e*stride), e < count, accurate (long double) -- the Stockham tables
+    size_t roots(uint64_t L, uint64_t count, uint64_t stride) {
+        size_t off = align();
+        const long double two_pi = 6.283185307179586476925286766559005768L;
+        for (uint64_t e = 0; e < count; e++) {
+            const uint64_t x = (e * stride) % L;
+            const long double ang = two_pi * ((long double)x / (long double)L);
+            put((double)cosl(ang), (double)(-sinl(ang)));
+        }
+        return off;
+    }
+    // omega(N,k), k < count, with the reference's own formula (CPU.c:644-651)
+    size_t reference_omega(uint64_t N, uint64_t count) {
+        size_t off = align();
+        for (uint64_t k = 0; k < count; k++)
+            put(cos(2.0 * M_PI / (double)N * (double)k), -sin(2.0 * M_PI / (double)N * (double)k));
+        return off;
+    }
+};
+
+struct TwoLevel {
+    size_t lo = 0, hi = 0;
+    uint32_t h = 0;
+};
+
+TwoLevel two_level(TableBuilder& tb, uint64_t L) {
+    TwoLevel t;
+    const int logl = ilog2u(L);
+    t.h = (uint32_t)((logl + 1) / 2);
+    t.lo = tb.roots(L, 1ull << t.h, 1);
+    t.hi = tb.roots(L, (L >> t.h) ? (L >> t.h) : 1, 1ull << t.h);
+    return t;
+}
+
+struct PassChoice {
+    int R, C;
+};
+
+int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out) {
+    out.clear();
+    if (M <= 1) return 0;
+    const int logm = ilog2u(M);
+    const int single_max = env_int("PIFFT_SINGLE_MAX_LOG", prec == 64 ? 13 : 14);
+    if (logm <= single_max) {
+        const int R = (int)M;
+        int C;
+        if (R <= 8) {
+            C = 64;
+        } else {
+            const int target = env_int(prec == 64 ? "PIFFT_SINGLE_ELEMS64" : "PIFFT_SINGLE_ELEMS32",
+                                       prec == 64 ? 4096 : 8192);
+            C = target / R;
+            if (C < 1) C = 1;
+            if (C > 16) C = 16;
+            while (C > 1 && (uint64_t)(C / 2) >= ntrans) C /= 2;
+            const int mx = max_lines(prec, R);
+            if (C > mx) C = mx;
+        }
+        out.push_back({R, C});
+        return 0;
+    }
+    const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32",
+                                 prec == 64 ? 10 : 11);
+    const int k = (logm + rmax_log - 1) / rmax_log;
+    const int base = logm / k, extra = logm % k;
+    for (int p = 0; p < k; p++) {
+        const int bits = base + (p < extra ? 1 : 0);
+        const int R = 1 << bits;
+        int C = env_int(prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", prec == 64 ? 8 : 16);
+        const int mx = max_lines(prec, R);
+        if (C > mx) C = mx;
+        if ((uint64_t)C > (M >> bits)) C = (int)(M >> bits);
+        if (!find_pass(prec, R, C)) return fail("no pass kernel for R=%d C=%d", R, C);
+        out.push_back({R, C});
+    }
+    return 0;
+}
+
+void release(pifft_plan* p) {
+    if (!p) return;
+    DeviceGuard g(p->device);
+    for (int b = BUF_W; b < NBUF; b++)
+        if (p->buf[b]) (void)hipFree(p->buf[b]);
+    if (p->d_tw) (void)hipFree(p->d_tw);
+    if (p->d_hin) (void)hipFree(p->d_hin);
+    if (p->d_hout) (void)hipFree(p->d_hout);
+    for (auto e : p->ev) (void)hipEventDestroy(e);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+int build_plan(pifft_plan* p) {
+    const size_t esz = p->esz;
+    const uint64_t ntrans = (uint64_t)p->batch * p->nq;  // local transforms
+    std::vector<PassChoice> passes;
+    if (plan_passes(p->m, p->prec, ntrans, passes)) return -1;
+
+    TableBuilder tb(esz);
+    // --- tree tables (w_N) ---
+    const bool need_tree = p->P > 1;
+    size_t tree_direct = 0;
+    TwoLevel tree2;
+    bool tree_is_direct = false;
+    if (need_tree) {
+        const int direct_max = env_int("PIFFT_TREE_DIRECT_MAX_LOG", 22);
+        if (p->log_n <= direct_max) {
+            tree_is_direct = true;
+            tree_direct = tb.reference_omega(p->n, p->n / 2);
+        } else {
+            tree2 = two_level(tb, p->n);
+        }
+    }
+    // --- pass tables ---
+    std::vector<size_t> tw_r(passes.size());
+    for (size_t i = 0; i < passes.size(); i++) {
+        size_t found = (size_t)-1;
+        for (size_t j = 0; j < i; j++)
+            if (passes[j].R == passes[i].R) found = tw_r[j];
+        tw_r[i] = (found != (size_t)-1) ? found : tb.roots(passes[i].R, passes[i].R, 1);
+    }
+    TwoLevel pass2;
+    if (passes.size() > 1) pass2 = two_level(tb, p->m);
+    tb.align();
+    p->tw_bytes = tb.blob.size() ? tb.blob.size() : 256;
+    HIPCHK(hipMalloc(&p->d_tw, p->tw_bytes));
+    if (!tb.blob.empty()) HIPCHK(hipMemcpy(p->d_tw, tb.blob.data(), tb.blob.size(), hipMemcpyHostToDevice));
+    auto twp = [&](size_t off) { return (const void*)((const char*)p->d_tw + off); };
+
+    // --- chain: [tree] [passes] [interleave] ---
+    struct Elem { std::vector<Step> steps; };
+    std::vector<Elem> chain;
+    const uint64_t M = p->m;
+    if (need_tree) {
+        Elem e;
+        if (p->lp <= 4) {
+            Step s;
+            s.kind = STEP_TREE;
+            s.tree_kind = 1;
+            const bool d = p->prec == 64;
+            static const void* tk64[5] = {nullptr, (const void*)&k_tree<double, 1>, (const void*)&k_tree<double, 2>,
+                                          (const void*)&k_tree<double, 3>, (const void*)&k_tree<double, 4>};
+            static const void* tk32[5] = {nullptr, (const void*)&k_tree<float, 1>, (const void*)&k_tree<float, 2>,
+                                          (const void*)&k_tree<float, 3>, (const void*)&k_tree<float, 4>};
+            s.fn = d ? tk64[p->lp] : tk32[p->lp];
+            s.ta.tw_direct = tree_is_direct ? twp(tree_direct) : nullptr;
+            s.ta.tw_lo = tree_is_direct ? nullptr : twp(tree2.lo);
+            s.ta.tw_hi = tree_is_direct ? nullptr : twp(tree2.hi);
+            s.ta.tw_h = tree2.h;
+            s.ta.in_bstride = p->n;
+            s.ta.out_bstride = (uint64_t)p->nq * M;
+            s.ta.total = (uint64_t)p->batch * M;
+            s.ta.log_m = (uint32_t)p->log_m;
+            s.ta.q0 = p->q0;
+            s.ta.nq = p->nq;
+            s.block = dim3(256);
+            s.grid = dim3((unsigned)((s.ta.total + 255) / 256));
+            s.bytes = (uint64_t)p->batch * (p->n + (uint64_t)p->nq * M) * esz;
+            e.steps.push_back(s);
+        } else {
+            // staged: per worker, one launch per radix-2 level (compact blocks)
+            p->bytes_ta = (size_t)p->batch * (p->n / 2) * esz;
+            p->bytes_tb = (size_t)p->batch * ((p->n / 4) ? p->n / 4 : 1) * esz;
+            const void* fn = p->prec == 64 ? (const void*)&k_tree_stage<double> : (const void*)&k_tree_stage<float>;
+            for (uint32_t q = p->q0; q < p->q0 + p->nq; q++) {
+                uint64_t size = p->n;
+                for (int t = 0; t < p->lp; t++, size /= 2) {
+                    Step s;
+                    s.kind = STEP_TREE;
+                    s.tree_kind = 2;
+                    s.fn = fn;
+                    const int iter = p->lp - t;                       // CPU.c:419
+                    const bool left = ((q >> (iter - 1)) % 2 == 0);  // CPU.c:429
+                    const bool lastlvl = (t == p->lp - 1);
+                    s.src = (t == 0) ? -1 : ((t % 2 == 1) ? BUF_TA : BUF_TB);  // -1: chain input
+                    s.dst = lastlvl ? -2 : ((t % 2 == 0) ? BUF_TA : BUF_TB);   // -2: chain output
+                    s.dst_off = lastlvl ? (uint64_t)(q - p->q0) * M : 0;
+                    s.tsa.tw_direct = tree_is_direct ? twp(tree_direct) : nullptr;
+                    s.tsa.tw_lo = tree_is_direct ? nullptr : twp(tree2.lo);
+                    s.tsa.tw_hi = tree_is_direct ? nullptr : twp(tree2.hi);
+                    s.tsa.tw_h = tree2.h;
+                    s.tsa.in_bstride = (t == 0) ? p->n : size;
+                    s.tsa.out_bstride = lastlvl ? (uint64_t)p->nq * M : size / 2;
+                    s.tsa.half = size / 2;
+                    s.tsa.log_half = (uint32_t)ilog2u(size / 2);
+                    s.tsa.total = (uint64_t)p->batch * (size / 2);
+                    s.tsa.t = (uint32_t)t;
+                    s.tsa.right = left ? 0u : 1u;
+                    s.block = dim3(256);
+                    s.grid = dim3((unsigned)((s.tsa.total + 255) / 256));
+                    s.bytes = (uint64_t)p->batch * (size + size / 2) * esz;
+                    e.steps.push_back(s);
+                }
+            }
+        }
+        p->tree_steps = (int)e.steps.size();
+        chain.push_back(e);
+    }
+    uint64_t ns = 1;
+    p->npasses = (int)passes.size();
+    for (size_t i = 0; i < passes.size(); i++) {
+        const PassKernel* k = find_pass(p->prec, passes[i].R, passes[i].C);
+        if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
+        Step s;
+        s.kind = STEP_PASS;
+        s.fn = k->fn;
+        const int logr = ilog2u((uint64_t)k->R);
+        s.pa.tw_r = twp(tw_r[i]);
+        s.pa.tw_lo = passes.size() > 1 ? twp(pass2.lo) : nullptr;
+        s.pa.tw_hi = passes.size() > 1 ? twp(pass2.hi) : nullptr;
+        s.pa.tw_h = pass2.h;
+        s.pa.in_bstride = (i == 0 && !need_tree) ? p->n : M;
+        s.pa.out_bstride = M;
+        s.pa.nlines = ntrans * (M >> logr);
+        s.pa.log_lb = (uint32_t)(p->log_m - logr);
+        s.pa.log_ns = (uint32_t)ilog2u(ns);
+        s.pa.tw_shift = (uint32_t)(p->log_m - ilog2u(ns) - logr);
+        s.block = dim3((unsigned)k->nt);
+        s.grid = dim3((unsigned)((s.pa.nlines + k->C - 1) / k->C));
+        s.lds = (size_t)k->lds_bytes;
+        s.bytes = 2 * ntrans * M * esz;
+        if (s.lds > 65536) (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
+        if (i < 8) {
+            p->radix[i] = k->R;
+            p->lines[i] = k->C;
+        }
+        ns *= (uint64_t)k->R;
+        Elem e;
+        e.steps.push_back(s);
+        chain.push_back(e);
+    }
+    if (p->natural && p->P > 1) {
+        Step s;
+        s.kind = STEP_INTERLEAVE;
+        s.fn = p->prec == 64 ? (const void*)&k_interleave<double> : (const void*)&k_interleave<float>;
+        s.il_total = (uint64_t)p->batch * p->n;
+        s.il_log_n = (uint32_t)p->log_n;
+        s.il_log_p = (uint32_t)p->lp;
+        s.block = dim3(256);
+        s.grid = dim3((unsigned)((s.il_total + 255) / 256));
+        s.bytes = 2 * s.il_total * esz;
+        Elem e;
+        e.steps.push_back(s);
+        chain.push_back(e);
+    }
+    if (chain.empty()) return fail("empty plan");
+    // destinations, backwards: last -> OUT, then W, OUT, W, ...
+    std::vector<int> dst(chain.size());
+    for (size_t i = chain.size(); i-- > 0;) dst[i] = ((chain.size() - 1 - i) % 2 == 0) ? BUF_OUT : BUF_W;
+    bool need_w = false;
+    for (size_t i = 0; i < chain.size(); i++) {
+        const int src = (i == 0) ? BUF_IN : dst[i - 1];
+        if (dst[i] == BUF_W || src == BUF_W) need_w = true;
+        for (auto& s : chain[i].steps) {
+            if (s.kind == STEP_TREE && s.tree_kind == 2) {
+                if (s.src == -1) s.src = src;
+                if (s.dst == -2) s.dst = dst[i];
+            } else {
+                s.src = src;
+                s.dst = dst[i];
+            }
+            p->steps.push_back(s);
+        }
+    }
+    if (p->steps.size() > 4096) return fail("plan too large (%zu launches)", p->steps.size());
+    p->bytes_w = need_w ? (size_t)p->batch * p->nq * M * esz : 0;
+    if (p->bytes_w) HIPCHK(hipMalloc(&p->buf[BUF_W], p->bytes_w));
+    if (p->bytes_ta) HIPCHK(hipMalloc(&p->buf[BUF_TA], p->bytes_ta));
+    if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
+    HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    p->ev.resize(p->steps.size() + 1);
+    for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
+    return 0;
+}
+
+int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint32_t count,
+           uint32_t batch, int prec, int device, int flags) {
+    if (!out) return fail("plan pointer is NULL");
+    *out = nullptr;
+    if (n < 2 || !is_pow2(n)) return fail("Invalid input size (should be 2^i for i>0)");
+    if (workers == 0 || !is_pow2(workers)) return fail("Invalid number of procs (should be 2^i for i>0)");
+    if (workers > n) return fail("More processors than inputs!");
+    if (count == 0 || !is_pow2(count) || first % count != 0 || (uint64_t)first + count > workers)
+        return fail("invalid worker range [%u, %u) of %u", first, first + count, workers);
+    if (batch == 0) return fail("batch must be >= 1");
+    if (prec != PIFFT_F32 && prec != PIFFT_F64) return fail("prec must be PIFFT_F32 or PIFFT_F64");
+    if (flags != PIFFT_OUT_NATURAL && flags != PIFFT_OUT_SLICES) return fail("unknown flags %d", flags);
+    if (flags == PIFFT_OUT_NATURAL && count != workers)
+        return fail("natural-order output needs all workers on one plan (use PIFFT_OUT_SLICES)");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail("no HIP device available");
+    if (device < 0 || device >= ndev) return fail("device %d out of range (%d devices)", device, ndev);
+    pifft_plan* p = new pifft_plan;
+    p->n = n;
+    p->P = workers;
+    p->q0 = first;
+    p->nq = count;
+    p->batch = batch;
+    p->prec = prec;
+    p->device = device;
+    p->flags = flags;
+    p->natural = (flags == PIFFT_OUT_NATURAL);
+    p->esz = prec == PIFFT_F64 ? 16 : 8;
+    p->lp = ilog2u(workers);
+    p->log_n = ilog2u(n);
+    p->log_m = p->log_n - p->lp;
+    p->m = n >> p->lp;
+    DeviceGuard g(device);
+    if (build_plan(p)) {
+        std::string keep = g_err;
+        release(p);
+        g_err = keep;
+        return -1;
+    }
+    *out = p;
+    return 0;
+}
+
+int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hipStream_t st) {
+    void* base[NBUF] = {const_cast<void*>(d_in), d_out, p->buf[BUF_W], p->buf[BUF_TA], p->buf[BUF_TB]};
+    const char* src = (const char*)base[s.src] + s.src_off * p->esz;
+    char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
+    hipError_t e = hipSuccess;
+    switch (s.kind) {
+        case STEP_PASS: {
+            PassArgs a = s.pa;
+            a.in = src;
+            a.out = dst;
+            void* args[] = {&a};
+            e = hipLaunchKernel(s.fn, s.grid, s.block, args, s.lds, st);
+            break;
+        }
+        case STEP_TREE: {
+            if (s.tree_kind == 1) {
+                TreeArgs a = s.ta;
+                a.in = src;
+                a.out = dst;
+                void* args[] = {&a};
+                e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
+            } else {
+                TreeStageArgs a = s.tsa;
+                a.in = src;
+                a.out = dst;
+                void* args[] = {&a};
+                e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
+            }
+            break;
+        }
+        case STEP_INTERLEAVE: {
+            const void* in = src;
+            void* o = dst;
+            uint64_t total = s.il_total;
+            uint32_t ln = s.il_log_n, lpp = s.il_log_p;
+            void* args[] = {&in, &o, &total, &ln, &lpp};
+            e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
+            break;
+        }
+        default:
+            return fail("bad step kind %d", s.kind);
+    }
+    if (e != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int check_buffers(const pifft_plan* p, const void* d_in, void* d_out) {
+    if (!p) return fail("plan is NULL");
+    if (!d_in || !d_out) return fail("NULL device buffer");
+    if (d_in == d_out) return fail("in-place execution is not supported (d_in == d_out)");
+    return 0;
+}
+
+uint64_t out_elems(const pifft_plan* p) { return (uint64_t)p->batch * p->nq * p->m; }
+
+// run every step with an event before each launch and after the last
+int run_timed(pifft_plan* p, const void* d_in, void* d_out, hipStream_t st, std::vector<float>& ms) {
+    const size_t ns = p->steps.size();
+    for (size_t i = 0; i < ns; i++) {
+        HIPCHK(hipEventRecord(p->ev[i], st));
+        if (launch_step(p, p->steps[i], d_in, d_out, st)) return -1;
+    }
+    HIPCHK(hipEventRecord(p->ev[ns], st));
+    HIPCHK(hipEventSynchronize(p->ev[ns]));
+    ms.assign(ns, 0.0f);
+    for (size_t i = 0; i < ns; i++) HIPCHK(hipEventElapsedTime(&ms[i], p->ev[i], p->ev[i + 1]));
+    return 0;
+}
+
+void stage_split(const pifft_plan* p, const std::vector<float>& ms, double* s1, double* s2) {
+    double a = 0, b = 0;
+    for (size_t i = 0; i < ms.size(); i++) (p->steps[i].kind == STEP_TREE ? a : b) += ms[i];
+    if (s1) *s1 = a;
+    if (s2) *s2 = b;
+}
+
+// device result (slice-major or natural) -> natural-order host positions
+void scatter_to_host(const pifft_plan* p, const char* res, char* host_out) {
+    const size_t esz = p->esz;
+    if (p->natural) {
+        memcpy(host_out, res, (size_t)p->batch * p->n * esz);
+        return;
+    }
+    const uint64_t M = p->m;
+    for (uint32_t bt = 0; bt < p->batch; bt++) {
+        for (uint32_t q = p->q0; q < p->q0 + p->nq; q++) {
+            const uint64_t r = bitrev(q, p->lp);
+            const char* s = res + ((uint64_t)bt * p->nq * M + (uint64_t)(q - p->q0) * M) * esz;
+            char* d = host_out + ((uint64_t)bt * p->n + r) * esz;
+            for (uint64_t k = 0; k < M; k++) memcpy(d + k * p->P * esz, s + k * esz, esz);
+        }
+    }
+}
+
+int ensure_host_staging(pifft_plan* p) {
+    if (!p->d_hin) HIPCHK(hipMalloc(&p->d_hin, (size_t)p->batch * p->n * p->esz));
+    if (!p->d_hout) HIPCHK(hipMalloc(&p->d_hout, (size_t)out_elems(p) * p->esz));
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+const char* pifft_last_error(void) { return g_err.c_str(); }
+
+int pifft_gpu_count(void) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        fail("hipGetDeviceCount: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return n;
+}
+
+int pifft_plan_create(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t batch, int prec) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return create(plan, n, workers, 0, workers, batch, prec, dev, PIFFT_OUT_NATURAL);
+}
+
+int pifft_plan_create_slices(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t first,
+                             uint32_t count, uint32_t batch, int prec, int device, int flags) {
+    return create(plan, n, workers, first, count, batch, prec, device, flags);
+}
+
+void pifft_plan_destroy(pifft_plan* plan) { release(plan); }
+
+int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
+    if (!p || !info) return fail("NULL argument");
+    memset(info, 0, sizeof *info);
+    info->n = p->n;
+    info->workers = p->P;
+    info->first_worker = p->q0;
+    info->num_workers = p->nq;
+    info->batch = p->batch;
+    info->prec = p->prec;
+    info->device = p->device;
+    info->flags = p->flags;
+    info->local_n = p->m;
+    info->in_elems = (uint64_t)p->batch * p->n;
+    info->out_elems = out_elems(p);
+    info->workspace_bytes = p->bytes_w + p->bytes_ta + p->bytes_tb + p->tw_bytes;
+    info->num_launches = (int)p->steps.size();
+    info->num_passes = p->npasses;
+    info->tree_launches = p->tree_steps;
+    for (int i = 0; i < 8; i++) {
+        info->radix[i] = p->radix[i];
+        info->lines[i] = p->lines[i];
+    }
+    for (size_t i = 0; i < p->steps.size() && i < 64; i++) {
+        info->launch_bytes[i] = p->steps[i].bytes;
+        info->launch_kind[i] = p->steps[i].kind;
+    }
+    return 0;
+}
+
+int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* stream) {
+    if (check_buffers(p, d_in, d_out)) return -1;
+    DeviceGuard g(p->device);
+    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
+    for (const auto& s : p->steps)
+        if (launch_step(p, s, d_in, d_out, st)) return -1;
+    return 0;
+}
+
+int pifft_execute_device_timed(pifft_plan* p, const void* d_in, void* d_out, void* stream,
+                               float* launch_ms, int max_launches) {
+    if (check_buffers(p, d_in, d_out)) return -1;
+    DeviceGuard g(p->device);
+    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
+    std::vector<float> ms;
+    if (run_timed(p, d_in, d_out, st, ms)) return -1;
+    if (launch_ms)
+        for (int i = 0; i < max_launches && i < (int)ms.size(); i++) launch_ms[i] = ms[i];
+    return 0;
+}
+
+int pifft_execute(pifft_plan* p, const void* host_in, void* host_out, double* ms1, double* ms2) {
+    return pifft_execute_group(&p, 1, host_in, host_out, ms1, ms2);
+}
+
+int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* host_out,
+                        double* ms1, double* ms2) {
+    if (!plans || np <= 0) return fail("no plans");
+    if (!host_in) return fail("host_in is NULL");
+    for (int i = 0; i < np; i++) {
+        if (!plans[i]) return fail("plan %d is NULL", i);
+        if (plans[i]->n != plans[0]->n || plans[i]->batch != plans[0]->batch ||
+            plans[i]->prec != plans[0]->prec)
+            return fail("plans of a group must share n, batch and precision");
+    }
+    // stage the input on every device (outside the timed region, like the
+    // reference's per-worker memcpy of the whole input, CPU.c:407)
+    for (int i = 0; i < np; i++) {
+        pifft_plan* p = plans[i];
+        DeviceGuard g(p->device);
+        if (ensure_host_staging(p)) return -1;
+        HIPCHK(hipMemcpyAsync(p->d_hin, host_in, (size_t)p->batch * p->n * p->esz, hipMemcpyHostToDevice,
+                              p->stream));
+        HIPCHK(hipStreamSynchronize(p->stream));
+    }
+    // launch all GPUs, then wait for all
+    for (int i = 0; i < np; i++) {
+        pifft_plan* p = plans[i];
+        DeviceGuard g(p->device);
+        const size_t ns = p->steps.size();
+        for (size_t s = 0; s < ns; s++) {
+            HIPCHK(hipEventRecord(p->ev[s], p->stream));
+            if (launch_step(p, p->steps[s], p->d_hin, p->d_hout, p->stream)) return -1;
+        }
+        HIPCHK(hipEventRecord(p->ev[ns], p->stream));
+    }
+    double t1 = 0, t2 = 0;
+    for (int i = 0; i < np; i++) {
+        pifft_plan* p = plans[i];
+        DeviceGuard g(p->device);
+        const size_t ns = p->steps.size();
+        HIPCHK(hipEventSynchronize(p->ev[ns]));
+        std::vector<float> ms(ns);
+        for (size_t s = 0; s < ns; s++) HIPCHK(hipEventElapsedTime(&ms[s], p->ev[s], p->ev[s + 1]));
+        double a, b;
+        stage_split(p, ms, &a, &b);
+        if (a + b > t1 + t2) {  // the slowest GPU sets the job's time
+            t1 = a;
+            t2 = b;
+        }
+    }
+    if (ms1) *ms1 = t1;
+    if (ms2) *ms2 = t2;
+    if (host_out) {
+        for (int i = 0; i < np; i++) {
+            pifft_plan* p = plans[i];
+            DeviceGuard g(p->device);
+            const size_t bytes = (size_t)out_elems(p) * p->esz;
+            p->host_tmp.resize(bytes);
+            HIPCHK(hipMemcpy(p->host_tmp.data(), p->d_hout, bytes, hipMemcpyDeviceToHost));
+            scatter_to_host(p, p->host_tmp.data(), (char*)host_out);
+        }
+    }
+    return 0;
+}
+
+int pifft_generate_device(void* d_x, uint64_t count, uint64_t n, uint64_t seed, uint64_t first,
+                          int prec, void* stream) {
+    if (!d_x) return fail("NULL buffer");
+    if (prec != PIFFT_F32 && prec != PIFFT_F64) return fail("bad precision");
+    if (count == 0) return 0;
+    const double scale = sqrt((double)n);
+    const dim3 blk(256), grd((unsigned)((count + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    if (prec == PIFFT_F64)
+        hipLaunchKernelGGL(k_generate<double>, grd, blk, 0, st, (cx<double>*)d_x, count, scale, seed, first);
+    else
+        hipLaunchKernelGGL(k_generate<float>, grd, blk, 0, st, (cx<float>*)d_x, count, scale, seed, first);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int pifft_interleave_device(const void* d_slices, void* d_out, uint64_t n, uint32_t workers,
+                            uint32_t batch, int prec, void* stream) {
+    if (!d_slices || !d_out || d_slices == d_out) return fail("bad buffers");
+    if (n < 2 || !is_pow2(n) || !workers || !is_pow2(workers) || workers > n) return fail("bad n/workers");
+    const uint64_t total = (uint64_t)batch * n;
+    const dim3 blk(256), grd((unsigned)((total + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t ln = (uint32_t)ilog2u(n), lpp = (uint32_t)ilog2u(workers);
+    if (prec == PIFFT_F64)
+        hipLaunchKernelGGL(k_interleave<double>, grd, blk, 0, st, (const cx<double>*)d_slices, (cx<double>*)d_out,
+                           total, ln, lpp);
+    else if (prec == PIFFT_F32)
+        hipLaunchKernelGGL(k_interleave<float>, grd, blk, 0, st, (const cx<float>*)d_slices, (cx<float>*)d_out,
+                           total, ln, lpp);
+    else
+        return fail("bad precision");
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int pifft_tree_device(pifft_plan* p, const void* d_in, void* d_seg, void* stream) {
+    if (check_buffers(p, d_in, d_seg)) return -1;
+    DeviceGuard g(p->device);
+    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
+    if (p->tree_steps == 0) {  // P == 1: the segment is the input
+        HIPCHK(hipMemcpyAsync(d_seg, d_in, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    for (int i = 0; i < p->tree_steps; i++) {
+        Step s = p->steps[i];
+        if (s.tree_kind == 1 || (s.dst != BUF_TA && s.dst != BUF_TB)) s.dst = BUF_OUT;
+        if (s.tree_kind == 1 || (s.src != BUF_TA && s.src != BUF_TB)) s.src = BUF_IN;
+        if (launch_step(p, s, d_in, d_seg, st)) return -1;
+    }
+    return 0;
+}
+
+}  // extern "C"

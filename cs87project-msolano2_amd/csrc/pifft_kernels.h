@@ -1,0 +1,445 @@
+// cs87project-msolano2_amd/csrc/pifft_kernels.h
+//
+// Hand-written gfx950 (CDNA4) kernels of the MI355X-native pi-FFT.  Device code
+// only; the host planner and the C-ABI live in pifft.hip.
+//
+// The reference computes, per worker q of P, a radix-2 DIF "tree" of log2 P
+// half-butterfly stages (CPU.c:419-448) followed by a radix-2 DIF FFT of its
+// N/P segment (the "cylinder", CPU.c:463-478), one butterfly per loop step with
+// a libm twiddle each (CPU.c:540-576, 644-651).  Here:
+//
+//  * k_tree   -- the tree stage, one thread per segment element: it loads the P
+//               inputs x[i + m*N/P] and evaluates the reference's radix-2 tree
+//               in registers in the reference's operation order (add/sub/mul of
+//               CPU.c:584-627, no FMA), keeping only the branches that lead to
+//               the requested workers.  With the host-built omega(N,k) table
+//               (CPU.c:644-651 formula) its output is bit-identical to the
+//               reference's post-tree segment.
+//  * k_tree_stage -- the same stage one radix-2 level per launch, for P > 16.
+//  * k_pass   -- one Stockham pass of the local N/P-point FFT: each workgroup
+//               stages C adjacent "lines" (sub-FFTs of length R, elements
+//               strided by M/R in HBM) in LDS, applies the inter-pass twiddle,
+//               runs the R-point FFT as radix-16 (plus one radix-2/4/8) stages
+//               with twiddles from a table, and writes the lines in Stockham
+//               (auto-sort) order.  Loads/stores are 16 B per lane for fp64 and
+//               coalesced across the C adjacent lines.
+//  * k_interleave -- slice-major worker outputs -> natural order.
+//  * k_generate   -- the synthetic splitmix64 input.
+//
+// Compile with -ffp-contract=off: the tree's bitwise parity with the
+// reference depends on every product and sum being rounded separately.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pifft {
+
+template <typename T>
+struct alignas(2 * sizeof(T)) cx {
+    T re, im;
+};
+
+template <typename T>
+__device__ __forceinline__ cx<T> cadd(cx<T> a, cx<T> b) {
+    return {a.re + b.re, a.im + b.im};
+}
+template <typename T>
+__device__ __forceinline__ cx<T> csub(cx<T> a, cx<T> b) {
+    return {a.re - b.re, a.im - b.im};
+}
+// CPU.c:620-627 order: re = ar*br - ai*bi, im = ar*bi + ai*br
+template <typename T>
+__device__ __forceinline__ cx<T> cmul(cx<T> a, cx<T> b) {
+    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+// a * (-i)
+template <typename T>
+__device__ __forceinline__ cx<T> mul_negi(cx<T> a) {
+    return {a.im, -a.re};
+}
+
+constexpr int ilog2c(uint64_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+
+// ---------------------------------------------------------------------------
+// Small forward DFTs in registers (natural order in and out), omega = e^{-2 pi i/q}
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void dft4(cx<T>& a0, cx<T>& a1, cx<T>& a2, cx<T>& a3) {
+    cx<T> t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    cx<T> t2 = cadd(a1, a3), t3 = mul_negi(csub(a1, a3));
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = cadd(t1, t3);
+    a3 = csub(t1, t3);
+}
+
+template <typename T>
+__device__ __forceinline__ void dft8(cx<T>* v) {
+    const T s = (T)0.70710678118654752440084436210484903928L;
+    cx<T> e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    cx<T> o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    dft4(e0, e1, e2, e3);
+    dft4(o0, o1, o2, o3);
+    o1 = {(o1.re + o1.im) * s, (o1.im - o1.re) * s};   // * w8^1 = (s, -s)
+    o2 = mul_negi(o2);                                 // * w8^2 = -i
+    o3 = {(o3.im - o3.re) * s, -((o3.re + o3.im) * s)}; // * w8^3 = (-s, -s)
+    v[0] = cadd(e0, o0);
+    v[4] = csub(e0, o0);
+    v[1] = cadd(e1, o1);
+    v[5] = csub(e1, o1);
+    v[2] = cadd(e2, o2);
+    v[6] = csub(e2, o2);
+    v[3] = cadd(e3, o3);
+    v[7] = csub(e3, o3);
+}
+
+template <typename T>
+__device__ __forceinline__ void dft16(cx<T>* v) {
+    const T c1 = (T)0.92387953251128675612818318939678828682L;  // cos(pi/8)
+    const T s1 = (T)0.38268343236508977172845998403039886676L;  // sin(pi/8)
+    const T s = (T)0.70710678118654752440084436210484903928L;
+    // n = 4 n1 + n2, k = k1 + 4 k2.  Column DFT4s over n1.
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++) dft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+    // v[4 k1 + n2] *= w16^(n2 k1)
+    const cx<T> w1 = {c1, -s1}, w2 = {s, -s}, w3 = {s1, -c1}, w6 = {-s, -s}, w9 = {-c1, s1};
+    v[5] = cmul(v[5], w1);
+    v[6] = cmul(v[6], w2);
+    v[7] = cmul(v[7], w3);
+    v[9] = cmul(v[9], w2);
+    v[10] = mul_negi(v[10]);
+    v[11] = cmul(v[11], w6);
+    v[13] = cmul(v[13], w3);
+    v[14] = cmul(v[14], w6);
+    v[15] = cmul(v[15], w9);
+    // row DFT4s over n2
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++) dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+    // v[4 k1 + k2] = X[k1 + 4 k2]: transpose the 4x4 (register renaming)
+    cx<T> t;
+#define PIFFT_SWP(a, b) t = v[a], v[a] = v[b], v[b] = t
+    PIFFT_SWP(1, 4);
+    PIFFT_SWP(2, 8);
+    PIFFT_SWP(3, 12);
+    PIFFT_SWP(6, 9);
+    PIFFT_SWP(7, 13);
+    PIFFT_SWP(11, 14);
+#undef PIFFT_SWP
+}
+
+template <int Q, typename T>
+__device__ __forceinline__ void dft(cx<T>* v) {
+    if constexpr (Q == 1) {
+    } else if constexpr (Q == 2) {
+        cx<T> a = v[0], b = v[1];
+        v[0] = cadd(a, b);
+        v[1] = csub(a, b);
+    } else if constexpr (Q == 4) {
+        dft4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (Q == 8) {
+        dft8(v);
+    } else {
+        static_assert(Q == 16, "radix");
+        dft16(v);
+    }
+}
+
+// two-level twiddle: w_M^E = hi[E >> h] * lo[E & (2^h - 1)]
+template <typename T>
+__device__ __forceinline__ cx<T> tw2(const cx<T>* __restrict__ lo, const cx<T>* __restrict__ hi,
+                                     uint32_t h, uint64_t E) {
+    const cx<T> a = lo[E & ((1ull << h) - 1)];
+    const cx<T> b = hi[E >> h];
+    return cmul(b, a);
+}
+
+// ---------------------------------------------------------------------------
+// Stockham pass
+// ---------------------------------------------------------------------------
+struct PassArgs {
+    const void* in;
+    void* out;
+    const void* tw_r;   // w_R^e, e < R
+    const void* tw_lo;  // two-level w_M
+    const void* tw_hi;
+    uint64_t in_bstride;  // elements between consecutive transforms (input)
+    uint64_t out_bstride;
+    uint64_t nlines;      // transforms * M/R
+    uint32_t log_lb;      // log2(M/R): lines per transform == element stride of a line
+    uint32_t log_ns;      // log2 Ns (product of the radices of the previous passes)
+    uint32_t tw_h;        // bits of the low twiddle table
+    uint32_t tw_shift;    // log2(M / (Ns R))
+};
+
+template <int R>
+struct PassShape {
+    static constexpr int Q = R >= 16 ? 16 : R;             // radix of the wide stages
+    static constexpr int LOGR = ilog2c(R);
+    static constexpr int NSTG = (LOGR + 3) / 4;             // radix-16 stages + 1 leading
+    static constexpr int Q0 = 1 << (LOGR - 4 * (NSTG - 1)); // leading radix 2/4/8/16
+    static constexpr int LS = R + R / 16 + 2;               // LDS line stride (elements)
+};
+
+template <int R, int C>
+struct PassCfg {
+    static constexpr int NT = C * R / PassShape<R>::Q;
+    static constexpr int lds_elems = PassShape<R>::NSTG > 1 ? C * PassShape<R>::LS : 0;
+};
+
+__device__ __forceinline__ int lds_idx(int c, int r, int LS) { return c * LS + r + (r >> 4); }
+
+template <typename T, int R, int C>
+__global__ __launch_bounds__((PassCfg<R, C>::NT)) void k_pass(PassArgs a) {
+    using C2 = cx<T>;
+    using S = PassShape<R>;
+    constexpr int Q = S::Q;
+    constexpr int NT = PassCfg<R, C>::NT;
+    constexpr int NSTG = S::NSTG;
+    constexpr int Q0 = S::Q0;
+    constexpr int LS = S::LS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
+    C2* lds = reinterpret_cast<C2*>(pifft_smem);
+
+    const C2* __restrict__ in = static_cast<const C2*>(a.in);
+    C2* __restrict__ out = static_cast<C2*>(a.out);
+    const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
+    const int tid = threadIdx.x;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t lb_mask = (1ull << a.log_lb) - 1;
+    const uint64_t ns_mask = (1ull << a.log_ns) - 1;
+
+    C2 v[Q];
+
+    // ---- stage 0: radix Q0, straight from HBM ------------------------------
+    {
+        constexpr int q = Q0, U = Q / q, NB = R / q;
+        const bool cfast = a.log_lb > 0;  // lines adjacent in memory -> lanes across lines
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int g = tid + u * NT;
+            const int c = cfast ? (g % C) : (g / NB);
+            const int b = cfast ? (g / C) : (g % NB);
+            const uint64_t line = tile * C + c;
+            const bool ok = line < a.nlines;
+            const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
+            const C2* src = in + bt * a.in_bstride + j;
+#pragma unroll
+            for (int k = 0; k < q; k++) {
+                const uint64_t r = (uint64_t)(b + k * NB);
+                v[u * q + k] = ok ? src[r << a.log_lb] : C2{(T)0, (T)0};
+            }
+            if (a.log_ns > 0) {  // inter-pass twiddle w_{Ns R}^{(j mod Ns) r}
+                const uint64_t jm = j & ns_mask;
+#pragma unroll
+                for (int k = 0; k < q; k++) {
+                    const uint64_t r = (uint64_t)(b + k * NB);
+                    const uint64_t E = (jm * r) << a.tw_shift;
+                    v[u * q + k] = cmul(v[u * q + k],
+                                        tw2(static_cast<const C2*>(a.tw_lo),
+                                            static_cast<const C2*>(a.tw_hi), a.tw_h, E));
+                }
+            }
+            dft<q>(&v[u * q]);
+            if constexpr (NSTG == 1) {
+                // single stage: outputs r' = k (b == 0) straight to HBM
+                if (ok) {
+                    const uint64_t jm = j & ns_mask;
+                    C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + S::LOGR)) + jm;
+#pragma unroll
+                    for (int k = 0; k < q; k++) {
+                        const uint64_t rp = (uint64_t)(b + k * NB);
+                        dst[rp << a.log_ns] = v[u * q + k];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < q; k++) lds[lds_idx(c, b * q + k, LS)] = v[u * q + k];
+            }
+        }
+    }
+    if constexpr (NSTG > 1) {
+    __syncthreads();
+
+    // ---- stages 1..NSTG-1: radix 16 through LDS ------------------------------
+#pragma unroll
+    for (int s = 1; s < NSTG; s++) {
+        constexpr int q = 16, NB = R / q;  // one butterfly per thread per line group
+        const int ns = Q0 << (4 * (s - 1));
+        const bool last = (s == NSTG - 1);
+        const bool cfast = last && a.log_ns > 0;
+        const int g = tid;
+        const int c = cfast ? (g % C) : (g / NB);
+        const int b = cfast ? (g / C) : (g % NB);
+#pragma unroll
+        for (int k = 0; k < q; k++) v[k] = lds[lds_idx(c, b + k * NB, LS)];
+        {   // w_{ns q}^{(b mod ns) k} = w_R^{(b mod ns) k R/(ns q)}
+            const int bm = b & (ns - 1);
+            const int scale = R / (ns * q);
+#pragma unroll
+            for (int k = 1; k < q; k++) v[k] = cmul(v[k], twr[bm * k * scale]);
+        }
+        dft<q>(v);
+        if (!last) {
+            __syncthreads();
+            const int base = (b / ns) * ns * q + (b & (ns - 1));
+#pragma unroll
+            for (int k = 0; k < q; k++) lds[lds_idx(c, base + k * ns, LS)] = v[k];
+            __syncthreads();
+        } else {
+            const uint64_t line = tile * C + c;
+            if (line < a.nlines) {
+                const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
+                const uint64_t jm = j & ns_mask;
+                C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + S::LOGR)) + jm;
+#pragma unroll
+                for (int k = 0; k < q; k++) {
+                    const uint64_t rp = (uint64_t)(b + k * NB);
+                    dst[rp << a.log_ns] = v[k];
+                }
+            }
+        }
+    }
+    }  // NSTG > 1
+}
+
+// ---------------------------------------------------------------------------
+// Tree ("funnel") stage
+// ---------------------------------------------------------------------------
+struct TreeArgs {
+    const void* in;
+    void* out;
+    const void* tw_direct;  // omega(N, e), e < N/2, reference formula; or null
+    const void* tw_lo;      // else two-level w_N
+    const void* tw_hi;
+    uint64_t in_bstride;    // N
+    uint64_t out_bstride;   // count * M
+    uint64_t total;         // transforms * M
+    uint32_t log_m;         // log2(N/P)
+    uint32_t tw_h;
+    uint32_t q0, nq;        // workers [q0, q0+nq)
+};
+
+template <typename T>
+__device__ __forceinline__ cx<T> tree_tw(const TreeArgs& a, uint64_t e) {
+    if (a.tw_direct) return static_cast<const cx<T>*>(a.tw_direct)[e];
+    return tw2(static_cast<const cx<T>*>(a.tw_lo), static_cast<const cx<T>*>(a.tw_hi), a.tw_h, e);
+}
+
+template <typename T, int LP>
+__global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
+    using C2 = cx<T>;
+    constexpr int P = 1 << LP;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= a.total) return;
+    const uint64_t M = 1ull << a.log_m;
+    const uint64_t i = gid & (M - 1), bt = gid >> a.log_m;
+    const C2* __restrict__ src = static_cast<const C2*>(a.in) + bt * a.in_bstride + i;
+    C2 v[P];
+#pragma unroll
+    for (int m = 0; m < P; m++) v[m] = src[(uint64_t)m << a.log_m];
+    const int q0 = (int)a.q0, q1 = (int)(a.q0 + a.nq);
+    // stage t (block size N >> t): CPU.c:419-448, one level of the radix-2 tree
+#pragma unroll
+    for (int t = 0; t < LP; t++) {
+        const int BS = P >> t, H = BS >> 1;
+#pragma unroll
+        for (int blk = 0; blk < (1 << t); blk++) {
+            const int lo = blk * BS;
+            // children [lo, lo+H) and [lo+H, lo+BS) of v-indices == worker ids below
+            const bool needL = (lo < q1) && (lo + H > q0);
+            const bool needR = (lo + H < q1) && (lo + BS > q0);
+#pragma unroll
+            for (int ml = 0; ml < H; ml++) {
+                const C2 x0 = v[lo + ml], x1 = v[lo + ml + H];
+                if (needL) v[lo + ml] = cadd(x0, x1);                        // butterfly_left
+                if (needR) {                                                 // butterfly_right
+                    const uint64_t e = (i + ((uint64_t)ml << a.log_m)) << t;  // b * N/size
+                    v[lo + ml + H] = cmul(csub(x0, x1), tree_tw<T>(a, e));
+                }
+            }
+        }
+    }
+    C2* __restrict__ dst = static_cast<C2*>(a.out) + bt * a.out_bstride + i;
+#pragma unroll
+    for (int q = 0; q < P; q++)
+        if (q >= q0 && q < q1) dst[(uint64_t)(q - q0) << a.log_m] = v[q];
+}
+
+// One radix-2 level of the tree for one worker (P > 16): compact block in,
+// compact half out (the reference's loop body, CPU.c:432-443, in parallel).
+struct TreeStageArgs {
+    const void* in;
+    void* out;
+    const void* tw_direct;
+    const void* tw_lo;
+    const void* tw_hi;
+    uint64_t in_bstride, out_bstride;
+    uint64_t half;   // size/2
+    uint64_t total;  // transforms * half
+    uint32_t log_half;
+    uint32_t t;      // level: twiddle exponent b << t
+    uint32_t right;
+    uint32_t tw_h;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_tree_stage(TreeStageArgs a) {
+    using C2 = cx<T>;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= a.total) return;
+    const uint64_t b = gid & (a.half - 1), bt = gid >> a.log_half;
+    const C2* src = static_cast<const C2*>(a.in) + bt * a.in_bstride;
+    const C2 x0 = src[b], x1 = src[b + a.half];
+    C2 r;
+    if (a.right) {
+        const uint64_t e = b << a.t;
+        C2 w;
+        if (a.tw_direct) w = static_cast<const C2*>(a.tw_direct)[e];
+        else w = tw2(static_cast<const C2*>(a.tw_lo), static_cast<const C2*>(a.tw_hi), a.tw_h, e);
+        r = cmul(csub(x0, x1), w);
+    } else {
+        r = cadd(x0, x1);
+    }
+    static_cast<C2*>(a.out)[bt * a.out_bstride + b] = r;
+}
+
+// ---------------------------------------------------------------------------
+// slice-major -> natural order: out[bt N + bitrev_P(q) + P k] = in[bt N + q M + k]
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_interleave(const cx<T>* __restrict__ in,
+                                                    cx<T>* __restrict__ out, uint64_t total,
+                                                    uint32_t log_n, uint32_t log_p) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= total) return;
+    const uint64_t n = 1ull << log_n;
+    const uint64_t bt = gid >> log_n, o = gid & (n - 1);
+    const uint64_t k = o >> log_p;
+    const uint32_t rr = (uint32_t)(o & ((1ull << log_p) - 1));
+    const uint32_t q = log_p ? (__builtin_bitreverse32(rr) >> (32 - log_p)) : 0u;
+    out[gid] = in[bt * n + ((uint64_t)q << (log_n - log_p)) + k];
+}
+
+// ---------------------------------------------------------------------------
+// synthetic input (bit-identical to oracle_generate_*)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t draw) {
+    uint64_t z = seed + (draw + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_generate(cx<T>* __restrict__ x, uint64_t count,
+                                                  double scale, uint64_t seed, uint64_t first) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= count) return;
+    const uint64_t d = 2 * (first + e);
+    const double ur = (double)(splitmix64(seed, d) >> 11) * 0x1.0p-53;
+    const double ui = (double)(splitmix64(seed, d + 1) >> 11) * 0x1.0p-53;
+    x[e] = cx<T>{(T)((2.0 * ur - 1.0) / scale), (T)((2.0 * ui - 1.0) / scale)};
+}
+
+}  // namespace pifft

@@ -1,0 +1,239 @@
+"""pifft.py -- Python (ctypes) view of libpifft.so, the MI355X pi-FFT C-ABI.
+
+Mirrors include/pifft.h one to one; used by bench.py, tests/ and
+__graft_entry__.  There is no fallback: if libpifft.so is missing or a call
+fails, a PifftError is raised with the library's own message (the reference
+prints its errors and exits non-zero, CPU.c:102-109).
+
+Device buffers are plain integer addresses (e.g. torch.Tensor.data_ptr()) and
+streams are raw hipStream_t handles (torch.cuda.Stream.cuda_stream) or None.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpifft.so")
+CLI_PATH = os.path.join(HERE, "pifft")
+
+F32, F64 = 32, 64
+OUT_NATURAL, OUT_SLICES = 0, 1
+KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave"}
+
+
+class PifftError(RuntimeError):
+    pass
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("workers", ctypes.c_uint32),
+        ("first_worker", ctypes.c_uint32),
+        ("num_workers", ctypes.c_uint32),
+        ("batch", ctypes.c_uint32),
+        ("prec", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("local_n", ctypes.c_uint64),
+        ("in_elems", ctypes.c_uint64),
+        ("out_elems", ctypes.c_uint64),
+        ("workspace_bytes", ctypes.c_uint64),
+        ("num_launches", ctypes.c_int32),
+        ("num_passes", ctypes.c_int32),
+        ("tree_launches", ctypes.c_int32),
+        ("radix", ctypes.c_int32 * 8),
+        ("lines", ctypes.c_int32 * 8),
+        ("launch_bytes", ctypes.c_uint64 * 64),
+        ("launch_kind", ctypes.c_int32 * 64),
+    ]
+
+
+# every symbol include/pifft.h declares, with its ctypes signature
+_P = ctypes.c_void_p
+_SIGS = {
+    "pifft_last_error": (ctypes.c_char_p, []),
+    "pifft_gpu_count": (ctypes.c_int, []),
+    "pifft_plan_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_uint64, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_int]),
+    "pifft_plan_create_slices": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_uint64, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "pifft_plan_destroy": (None, [_P]),
+    "pifft_plan_get_info": (ctypes.c_int, [_P, ctypes.POINTER(PlanInfo)]),
+    "pifft_execute_device": (ctypes.c_int, [_P, _P, _P, _P]),
+    "pifft_execute_device_timed": (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_float),
+                                                  ctypes.c_int]),
+    "pifft_execute": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]),
+    "pifft_execute_group": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _P,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "pifft_generate_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_int, _P]),
+    "pifft_interleave_device": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_int, _P]),
+    "pifft_tree_device": (ctypes.c_int, [_P, _P, _P, _P]),
+}
+SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def build(quiet: bool = True) -> None:
+    """hipcc --offload-arch=gfx950 -> libpifft.so, gcc -> the pifft CLI (in-tree)."""
+    subprocess.run(["make", "-C", HERE, "all"], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PifftError(f"{LIB_PATH} not built (run __graft_entry__.build() or make -C {HERE})")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7;
+        # loading torch first makes libpifft.so bind to that same runtime (its
+        # NEEDED soname resolves to the already-loaded library).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().pifft_last_error().decode()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise PifftError(f"{what}: {last_error()}")
+
+
+def gpu_count() -> int:
+    n = lib().pifft_gpu_count()
+    if n < 0:
+        raise PifftError(last_error())
+    return n
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    return int(stream)
+
+
+class Plan:
+    """One GPU's share of an N-point, P-worker pi-FFT (pifft_plan)."""
+
+    def __init__(self, n: int, workers: int = 1, batch: int = 1, prec: int = F64, *,
+                 first: int = 0, count: int | None = None, device: int | None = None,
+                 flags: int | None = None):
+        h = _P()
+        if count is None and device is None and flags is None and first == 0:
+            _check(lib().pifft_plan_create(ctypes.byref(h), n, workers, batch, prec), "pifft_plan_create")
+        else:
+            count = workers if count is None else count
+            device = 0 if device is None else device
+            if flags is None:
+                flags = OUT_NATURAL if count == workers else OUT_SLICES
+            _check(lib().pifft_plan_create_slices(ctypes.byref(h), n, workers, first, count, batch, prec,
+                                                  device, flags), "pifft_plan_create_slices")
+        self._h = h
+        self.info = self._info()
+
+    def _info(self) -> PlanInfo:
+        info = PlanInfo()
+        _check(lib().pifft_plan_get_info(self._h, ctypes.byref(info)), "pifft_plan_get_info")
+        return info
+
+    @property
+    def handle(self):
+        return self._h
+
+    def describe(self) -> dict:
+        i = self.info
+        nl = i.num_launches
+        return {
+            "n": i.n, "workers": i.workers, "first_worker": i.first_worker, "num_workers": i.num_workers,
+            "batch": i.batch, "prec": i.prec, "local_n": i.local_n, "in_elems": i.in_elems,
+            "out_elems": i.out_elems, "workspace_bytes": i.workspace_bytes, "num_launches": nl,
+            "num_passes": i.num_passes, "tree_launches": i.tree_launches,
+            "radix": list(i.radix[: i.num_passes]), "lines": list(i.lines[: i.num_passes]),
+            "launch_bytes": list(i.launch_bytes[: min(nl, 64)]),
+            "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, 64)]],
+        }
+
+    def execute_device(self, d_in: int, d_out: int, stream=None) -> None:
+        _check(lib().pifft_execute_device(self._h, d_in, d_out, _stream(stream)), "pifft_execute_device")
+
+    def execute_device_timed(self, d_in: int, d_out: int, stream=None) -> list[float]:
+        n = self.info.num_launches
+        buf = (ctypes.c_float * max(n, 1))()
+        _check(lib().pifft_execute_device_timed(self._h, d_in, d_out, _stream(stream), buf, n),
+               "pifft_execute_device_timed")
+        return list(buf[:n])
+
+    def execute(self, host_in, host_out=None):
+        """numpy in -> natural-order numpy out (only this plan's bins written)."""
+        import numpy as np
+        host_in = np.ascontiguousarray(host_in)
+        t1, t2 = ctypes.c_double(), ctypes.c_double()
+        out_ptr = None if host_out is None else host_out.ctypes.data
+        _check(lib().pifft_execute(self._h, host_in.ctypes.data, out_ptr, ctypes.byref(t1), ctypes.byref(t2)),
+               "pifft_execute")
+        return t1.value, t2.value
+
+    def tree_device(self, d_in: int, d_seg: int, stream=None) -> None:
+        _check(lib().pifft_tree_device(self._h, d_in, d_seg, _stream(stream)), "pifft_tree_device")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            lib().pifft_plan_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def execute_group(plans, host_in, host_out=None):
+    import numpy as np
+    host_in = np.ascontiguousarray(host_in)
+    arr = (_P * len(plans))(*[p.handle.value for p in plans])
+    t1, t2 = ctypes.c_double(), ctypes.c_double()
+    out_ptr = None if host_out is None else host_out.ctypes.data
+    _check(lib().pifft_execute_group(arr, len(plans), host_in.ctypes.data, out_ptr, ctypes.byref(t1),
+                                     ctypes.byref(t2)), "pifft_execute_group")
+    return t1.value, t2.value
+
+
+def generate_device(d_x: int, count: int, n: int, prec: int, seed: int = 0x5EED, first: int = 0,
+                    stream=None) -> None:
+    _check(lib().pifft_generate_device(d_x, count, n, seed, first, prec, _stream(stream)),
+           "pifft_generate_device")
+
+
+def interleave_device(d_slices: int, d_out: int, n: int, workers: int, batch: int, prec: int,
+                      stream=None) -> None:
+    _check(lib().pifft_interleave_device(d_slices, d_out, n, workers, batch, prec, _stream(stream)),
+           "pifft_interleave_device")
+
+
+def header_symbols(header_path: str | None = None) -> list[str]:
+    """Function names declared in include/pifft.h (for the ABI export test)."""
+    import re
+    header_path = header_path or os.path.join(os.path.dirname(HERE), "include", "pifft.h")
+    text = open(header_path).read()
+    return sorted(set(re.findall(r"\b(pifft_[a-z_]+)\s*\(", text)))

@@ -1,0 +1,66 @@
+"""pifft_dist.py -- the multi-GPU (one process per GPU) side of the pi-FFT.
+
+The reference splits the transform over P workers that never exchange data
+(CPU.c:336-360: P pinned pthreads, each writing its own output bins).  Here one
+worker range lives on each GPU/rank:
+
+  * worker_range(rank, world, P): rank r computes workers [r P/W, (r+1) P/W)
+    (the reference's Pi, CPU.c:336) -- no collective on the data path;
+  * the only optional exchange is the final all-gather of the slices
+    (torch.distributed all_gather over RCCL/xGMI, or gloo on CPU) followed by
+    the stride-P interleave (interleave_slices / pifft_interleave_device);
+  * max_over_ranks: the job's time is the slowest rank's.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def worker_range(rank: int, world: int, workers: int) -> tuple[int, int]:
+    if world < 1 or workers % world:
+        raise ValueError(f"{workers} workers cannot be split over {world} ranks")
+    per = workers // world
+    return rank * per, per
+
+
+def bitrev(x: int, bits: int) -> int:
+    r = 0
+    for _ in range(bits):
+        r = (r << 1) | (x & 1)
+        x >>= 1
+    return r
+
+
+def interleave_slices(slices: np.ndarray) -> np.ndarray:
+    """(P, M) slice-major worker outputs -> natural order: out[bitrev(q) + P k] = slices[q, k]."""
+    P, M = slices.shape
+    bits = P.bit_length() - 1
+    out = np.empty(P * M, dtype=slices.dtype)
+    for q in range(P):
+        out[bitrev(q, bits)::P] = slices[q]
+    return out
+
+
+def slice_of_natural(X: np.ndarray, P: int, q: int) -> np.ndarray:
+    """Worker q's bins of a natural-order result: X[bitrev(q) + P k], k < N/P."""
+    return X[bitrev(q, P.bit_length() - 1)::P]
+
+
+def allgather_slices(local, group=None):
+    """All-gather equal-size per-rank slice tensors (rank order)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local.contiguous(), group=group)
+    return torch.cat(parts)
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,144 @@
+/*
+ * include/pifft.h -- C-ABI of libpifft.so, the MI355X-native "pi" FFT.
+ *
+ * Drop-in boundary for the reference CPU path
+ *   benchmark/fourier/parallel/pi/cpu/pthreads/fourier-parallel-pi-cpu-pthreads.c
+ * (abbreviated CPU.c).  The reference has no library API: its C entry points
+ * are setup_from_args (CPU.c:125), run (CPU.c:312) and the per-worker
+ * run_thread (CPU.c:388), which together compute a radix-2 DIF FFT split over
+ * P workers that never exchange data.  This header is the shim those entry
+ * points call instead (see cs87project-msolano2_amd/csrc/host/pifft_cli.c for
+ * the C host that keeps the reference CLI, and INTEGRATION.md for the one-line
+ * change to the reference's run()).
+ *
+ * Conventions (mirroring the reference): functions return 0 on success and
+ * -1 on error (CPU.c:102-109, 208-210); the error text is then available from
+ * pifft_last_error() (the reference prints to stderr instead).  No C++
+ * exception crosses this boundary.  Plain pointers and sizes only.
+ *
+ * Data: interleaved complex, {float re, im} (PIFFT_F32, the reference's data_t,
+ * CPU.c:33-36) or {double re, im} (PIFFT_F64, the reference built with
+ * -Dfloat=double).  Transform: unnormalised forward DFT
+ * X[k] = sum_n x[n] e^{-2 pi i nk/N}, natural-order input and output (the
+ * reference's `out` after its bit-reversed scatter, CPU.c:496-499).
+ *
+ * Workers: worker q of P owns the natural-order output bins
+ *   bitrev_{log2 P}(q) + P*k,  k < N/P
+ * (the reference's segment q of its bit-reversed scratch).  A plan computes a
+ * contiguous range of workers [first, first+count) on one GPU; a plan with
+ * count == P on one GPU is the whole transform.
+ */
+#ifndef PIFFT_H
+#define PIFFT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PIFFT_F32 32
+#define PIFFT_F64 64
+
+/* plan flags */
+#define PIFFT_OUT_NATURAL 0 /* device output in natural order (needs count == P)   */
+#define PIFFT_OUT_SLICES 1  /* device output slice-major: worker q's N/P bins
+                               Z_q[k] = X[bitrev(q) + P k] contiguous, q = first.. */
+
+typedef struct pifft_plan pifft_plan;
+
+typedef struct pifft_plan_info {
+    uint64_t n;              /* transform length N                                */
+    uint32_t workers;        /* P                                                 */
+    uint32_t first_worker;   /* workers [first_worker, first_worker+num_workers)  */
+    uint32_t num_workers;
+    uint32_t batch;          /* independent transforms per execute               */
+    int32_t prec;            /* PIFFT_F32 | PIFFT_F64                             */
+    int32_t device;          /* HIP device ordinal                                */
+    int32_t flags;
+    uint64_t local_n;        /* M = N/P, the per-worker ("cylinder") FFT length   */
+    uint64_t in_elems;       /* complex elements expected at d_in  (batch*N)      */
+    uint64_t out_elems;      /* complex elements written to d_out                 */
+    uint64_t workspace_bytes;
+    int32_t num_launches;    /* kernel launches per execute                        */
+    int32_t num_passes;      /* Stockham passes of the local FFT                   */
+    int32_t tree_launches;   /* launches of the tree ("funnel") stage              */
+    int32_t radix[8];        /* LDS-resident sub-FFT length of each pass           */
+    int32_t lines[8];        /* columns per workgroup of each pass                 */
+    uint64_t launch_bytes[64]; /* algorithmic HBM bytes of each launch (read+write,
+                                  twiddle tables excluded)                         */
+    int32_t launch_kind[64]; /* 1 tree, 2 pass, 3 interleave                      */
+} pifft_plan_info;
+
+/* Last error message of the calling thread ("" if none). */
+const char* pifft_last_error(void);
+
+/* Number of visible HIP devices, or -1 (replaces how-many-concurrent-blocks.cu
+ * and the core count check of CPU.c:200, 835-837). */
+int pifft_gpu_count(void);
+
+/* Whole transform on the current device: all P workers, natural-order output
+ * (the reference's run(), CPU.c:312-380).  n, workers: powers of two, 2 <= n,
+ * 1 <= workers <= n (CPU.c:139-198).  batch >= 1 transforms laid out back to
+ * back.  prec: PIFFT_F32 or PIFFT_F64. */
+int pifft_plan_create(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t batch,
+                      int prec);
+
+/* Workers [first, first+count) of a P-worker split on `device` (one GPU of a
+ * multi-GPU job; the reference's run_thread for each of those Pi).  count must
+ * be a power of two dividing first.  flags: PIFFT_OUT_NATURAL (only when
+ * count == workers) or PIFFT_OUT_SLICES. */
+int pifft_plan_create_slices(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t first,
+                             uint32_t count, uint32_t batch, int prec, int device, int flags);
+
+void pifft_plan_destroy(pifft_plan* plan);
+
+int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
+
+/* Device boundary: d_in holds info.in_elems complex values, d_out receives
+ * info.out_elems (d_in != d_out; neither is freed).  Asynchronous on `stream`
+ * (a hipStream_t, NULL = the plan's own stream). */
+int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* stream);
+
+/* As pifft_execute_device, but records a HIP event before every launch and
+ * after the last one on `stream`, waits, and returns each launch's duration in
+ * launch_ms[0 .. min(info.num_launches, max_launches)). */
+int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, void* stream,
+                               float* launch_ms, int max_launches);
+
+/* Host boundary, the reference's run() shape: copies host_in (batch*N values)
+ * to the device (untimed), runs, and if host_out != NULL writes this plan's
+ * bins at their natural-order positions of host_out (batch*N values; other
+ * positions untouched -- the reference's workers write disjoint `out` entries,
+ * CPU.c:496-499).  ms_stage1 / ms_stage2 receive the device time of the tree
+ * stage and of the rest (the reference's two timers, CPU.c:414-481). */
+int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double* ms_stage1,
+                  double* ms_stage2);
+
+/* Several plans (normally one per GPU) run concurrently from one host thread:
+ * the P-GPU no-communication split.  Stage times are the max over plans. */
+int pifft_execute_group(pifft_plan** plans, int nplans, const void* host_in, void* host_out,
+                        double* ms_stage1, double* ms_stage2);
+
+/* Synthetic input on the device: element e (count of them, starting at global
+ * element index `first`) = splitmix64(seed) draws 2e, 2e+1 mapped to
+ * (2u-1)/sqrt(n) -- bit-identical to the host generator of the test oracle. */
+int pifft_generate_device(void* d_x, uint64_t count, uint64_t n, uint64_t seed, uint64_t first,
+                          int prec, void* stream);
+
+/* Slice-major -> natural order: out[bitrev_{log2 P}(q) + P k] = slices[q M + k]
+ * for all P workers (M = n/P), `batch` transforms (used after an all-gather). */
+int pifft_interleave_device(const void* d_slices, void* d_out, uint64_t n, uint32_t workers,
+                            uint32_t batch, int prec, void* stream);
+
+/* Tree ("funnel") stage only, for parity checks: writes worker q's N/P segment
+ * after the log2 P half-butterfly stages (the reference's tmp_in segment after
+ * CPU.c:419-448) for the plan's workers, slice-major. */
+int pifft_tree_device(pifft_plan* plan, const void* d_in, void* d_seg, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PIFFT_H */

@@ -1,0 +1,50 @@
+"""The C-ABI library (libpifft.so) loads and exports every symbol of
+include/pifft.h; argument validation follows the reference's rules and
+messages (CPU.c:139-198).  No compute call is made (runs without a GPU)."""
+import ctypes
+import os
+
+import pytest
+
+import pifft
+
+
+def test_library_is_built_for_gfx950():
+    assert os.path.exists(pifft.LIB_PATH), "run __graft_entry__.build()"
+    blob = open(pifft.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_exports_every_header_symbol():
+    L = ctypes.CDLL(pifft.LIB_PATH)
+    declared = pifft.header_symbols()
+    assert set(declared) == set(pifft.SYMBOLS), "pifft.py signatures out of sync with include/pifft.h"
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+@pytest.mark.parametrize("n,P,msg", [
+    (3, 1, "Invalid input size"),
+    (1, 1, "Invalid input size"),
+    (16, 3, "Invalid number of procs"),
+    (16, 0, "Invalid number of procs"),
+    (16, 32, "More processors than inputs!"),
+])
+def test_validation_messages(n, P, msg):
+    with pytest.raises(pifft.PifftError, match=msg):
+        pifft.Plan(n, P, 1, pifft.F64)
+
+
+def test_bad_precision_and_ranges():
+    with pytest.raises(pifft.PifftError, match="prec"):
+        pifft.Plan(16, 1, 1, 48)
+    with pytest.raises(pifft.PifftError, match="worker range"):
+        pifft.Plan(16, 4, 1, pifft.F64, first=1, count=2)
+    with pytest.raises(pifft.PifftError, match="natural-order"):
+        pifft.Plan(16, 4, 1, pifft.F64, first=0, count=2, flags=pifft.OUT_NATURAL)
+
+
+def test_error_string_roundtrip():
+    with pytest.raises(pifft.PifftError):
+        pifft.Plan(12, 1)
+    assert "Invalid input size" in pifft.last_error()

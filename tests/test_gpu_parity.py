@@ -1,0 +1,348 @@
+"""HIP path vs the reference, through the C-ABI (libpifft.so) on an MI355X.
+
+Oracle: the reference's own outputs (tests/golden/, bitwise-pinned) and the C
+restatement (oracle/) on the same seeded inputs.  Bars (BASELINE.json
+north_star): relative L2 error <= 1e-12 (fp64) and <= 1e-5*log2(N) (fp32);
+index permutation exact (checked per bin as well as in L2); the tree stage
+and the input generator bit-exact.  Sizes beyond the oracle's reach are checked
+through size-independent properties (double-transform identity, Parseval,
+linearity, direct DFT bins, P-split consistency).
+"""
+import hashlib
+import math
+import os
+
+import numpy as np
+import pytest
+
+import pifft
+import pifft_dist
+import pifft_oracle as oracle
+from golden_io import load_fft, load_tree, manifest, rel_l2
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+DT = {"f32": np.complex64, "f64": np.complex128}
+PREC = {"f32": pifft.F32, "f64": pifft.F64}
+TDT = {np.complex64: torch.complex64, np.complex128: torch.complex128}
+
+
+def tol(suf, n):
+    return 1e-12 if suf == "f64" else 1e-5 * math.log2(n)
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to("cuda")
+
+
+def run(plan, x, slices=False):
+    """Execute a plan on a host array through device buffers; returns host result."""
+    d_in = dev(x)
+    info = plan.info
+    d_out = torch.empty(info.out_elems, dtype=d_in.dtype, device="cuda")
+    plan.execute_device(d_in.data_ptr(), d_out.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    return d_out.cpu().numpy()
+
+
+def assert_bins_close(got, want, suf, n):
+    err = rel_l2(got, want)
+    assert err <= tol(suf, n), f"rel-L2 {err:.3e} > {tol(suf, n):.1e}"
+    # permutation: every bin must be closer to its own reference value than the
+    # spread of the spectrum (a swapped index would show as an O(1) error)
+    scale = np.linalg.norm(want) / math.sqrt(len(want))
+    assert np.max(np.abs(got - want)) <= max(50 * tol(suf, n), 1e-9) * scale * math.sqrt(len(want))
+
+
+def test_device_visible():
+    assert torch.cuda.is_available()
+    assert pifft.gpu_count() >= 1
+
+
+# ------------------------------------------------------------------ golden ---
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("n", [2, 4, 8, 16, 64, 1024, 4096])
+def test_golden_all_workers_natural(suf, n):
+    x, X = load_fft(suf, n)
+    for P in (1, 2, 4, 8, n):
+        if P > n:
+            continue
+        plan = pifft.Plan(n, P, 1, PREC[suf])
+        got = run(plan, x)
+        assert_bins_close(got, X, suf, n)
+
+
+@pytest.mark.parametrize("suf", list(DT))
+def test_reference_known_answer_exact(suf):
+    # CPU.c:251-260,689-705: exact float equality
+    x = np.array([0, 1, 0, 1, 0, 1, 0, 1], dtype=DT[suf])
+    for P in (1, 2, 4, 8):
+        got = run(pifft.Plan(8, P, 1, PREC[suf]), x)
+        assert np.array_equal(got, np.array([4, 0, 0, 0, -4, 0, 0, 0], dtype=DT[suf]))
+
+
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("n,P", [(64, 8), (64, 2), (1024, 4), (4096, 16), (256, 256)])
+def test_tree_stage_bitwise_vs_reference(suf, n, P):
+    """k_tree / k_tree_stage == the reference's post-tree segments, bit for bit."""
+    x, segs = load_tree(suf, n, P)
+    plan = pifft.Plan(n, P, 1, PREC[suf], first=0, count=P, device=0, flags=pifft.OUT_SLICES)
+    d_in = dev(x)
+    d_seg = torch.empty(n, dtype=d_in.dtype, device="cuda")
+    plan.tree_device(d_in.data_ptr(), d_seg.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = d_seg.cpu().numpy().reshape(P, n // P)
+    assert got.tobytes() == segs.tobytes()
+    # and for single-worker plans (one GPU of a P-GPU job)
+    for q in (0, P - 1, P // 2):
+        p1 = pifft.Plan(n, P, 1, PREC[suf], first=q, count=1, device=0)
+        d1 = torch.empty(n // P, dtype=d_in.dtype, device="cuda")
+        p1.tree_device(d_in.data_ptr(), d1.data_ptr(), torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert d1.cpu().numpy().tobytes() == segs[q].tobytes(), f"q={q}"
+
+
+@pytest.mark.parametrize("suf", list(DT))
+def test_generator_bitwise(suf):
+    n = 1 << 16
+    d = torch.empty(n, dtype=TDT[DT[suf]], device="cuda")
+    pifft.generate_device(d.data_ptr(), n, n, PREC[suf], seed=0x5EED, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert d.cpu().numpy().tobytes() == oracle.generate(n, DT[suf], 0x5EED).tobytes()
+    # the N=2^20 fixture digest
+    big = manifest()["big"][suf]
+    n = big["n"]
+    d = torch.empty(n, dtype=TDT[DT[suf]], device="cuda")
+    pifft.generate_device(d.data_ptr(), n, n, PREC[suf], stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest() == big["sha256_x"]
+
+
+# ------------------------------------------------ the BASELINE configs (1-3) ---
+@pytest.mark.parametrize("P", [1, 8])
+def test_config1_2_n2e20_fp64(P):
+    """C1 (P=1) and C2 (P=8 on one GPU), against the oracle on identical input."""
+    n = 1 << 20
+    x = oracle.generate(n, np.complex128)
+    want = oracle.fft(x, P=P, nthreads=8)
+    got = run(pifft.Plan(n, P, 1, pifft.F64), x)
+    assert_bins_close(got, want, "f64", n)
+
+
+def test_config2_slices_per_gpu_fp64():
+    """C2 as 8 single-worker plans (one per GPU in the 8-GPU job): each owns
+    bins bitrev(q) + 8k, and their all-gather + interleave is the transform."""
+    n, P = 1 << 20, 8
+    x = oracle.generate(n, np.complex128)
+    want = oracle.fft(x, P=1, nthreads=1)
+    slices = []
+    for q in range(P):
+        plan = pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0)
+        s = run(plan, x)
+        assert_bins_close(s, pifft_dist.slice_of_natural(want, P, q), "f64", n)
+        slices.append(s)
+    assert_bins_close(pifft_dist.interleave_slices(np.stack(slices)), want, "f64", n)
+    # device interleave of the gathered slices
+    d_sl = dev(np.concatenate(slices))
+    d_out = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.interleave_device(d_sl.data_ptr(), d_out.data_ptr(), n, P, 1, pifft.F64, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert d_out.cpu().numpy().tobytes() == pifft_dist.interleave_slices(np.stack(slices)).tobytes()
+
+
+def test_config3_batched_fp32_4096x4096():
+    n, b = 4096, 4096
+    x = oracle.generate(n, np.complex64, count=n * b)
+    plan = pifft.Plan(n, 1, b, pifft.F32)
+    assert plan.describe()["num_passes"] == 1
+    got = run(plan, x).reshape(b, n)
+    xs = x.reshape(b, n)
+    for i in (0, 1, 2047, 4095):
+        assert_bins_close(got[i], oracle.fft(xs[i]), "f32", n)
+    # whole batch against a float64 numpy FFT (same tolerance)
+    assert rel_l2(got, np.fft.fft(xs.astype(np.complex128), axis=1)) <= tol("f32", n)
+
+
+# ------------------------------------------------------------- sweeps/edges ---
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("logn", list(range(1, 23)))
+def test_size_sweep_vs_oracle(suf, logn):
+    n = 1 << logn
+    x = oracle.generate(n, DT[suf], seed=1234 + logn)
+    want = oracle.fft(x, P=1)
+    for P in sorted({1, 2, min(n, 8), min(n, 32)}):
+        got = run(pifft.Plan(n, P, 1, PREC[suf]), x)
+        assert_bins_close(got, want, suf, n)
+
+
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("n,P,b", [(2, 2, 3), (16, 16, 5), (1024, 4, 7), (1 << 15, 8, 3), (1 << 16, 64, 2),
+                                   (64, 64, 2), (8192, 1, 33), (1 << 14, 2, 4)])
+def test_batched_and_many_workers(suf, n, P, b):
+    x = oracle.generate(n, DT[suf], seed=99, count=n * b)
+    got = run(pifft.Plan(n, P, b, PREC[suf]), x).reshape(b, n)
+    for i in range(b):
+        assert_bins_close(got[i], oracle.fft(x[i * n:(i + 1) * n]), suf, n)
+
+
+@pytest.mark.parametrize("suf", list(DT))
+def test_worker_ranges_slices_layout(suf):
+    n, P = 1 << 12, 16
+    x = oracle.generate(n, DT[suf])
+    want = oracle.fft(x)
+    for first, count in [(0, 16), (0, 8), (8, 8), (4, 4), (12, 2), (5, 1)]:
+        plan = pifft.Plan(n, P, 1, PREC[suf], first=first, count=count, device=0, flags=pifft.OUT_SLICES)
+        got = run(plan, x).reshape(count, n // P)
+        for j in range(count):
+            assert_bins_close(got[j], pifft_dist.slice_of_natural(want, P, first + j), suf, n)
+
+
+def test_host_boundary_and_group():
+    """pifft_execute (the reference run() shape) and pifft_execute_group (the
+    multi-GPU job from one host thread; here 4 plans share device 0)."""
+    n, P = 1 << 14, 4
+    x = oracle.generate(n, np.complex128)
+    want = oracle.fft(x)
+    out = np.zeros_like(x)
+    t1, t2 = pifft.Plan(n, P, 1, pifft.F64).execute(x, out)
+    assert t1 >= 0 and t2 > 0
+    assert_bins_close(out, want, "f64", n)
+    plans = [pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0) for q in range(P)]
+    out2 = np.zeros_like(x)
+    pifft.execute_group(plans, x, out2)
+    assert_bins_close(out2, want, "f64", n)
+
+
+def test_timed_execution_reports_every_launch():
+    n = 1 << 20
+    plan = pifft.Plan(n, 8, 1, pifft.F64)
+    d = plan.describe()
+    x = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=torch.cuda.current_stream())
+    y = torch.empty(n, dtype=torch.complex128, device="cuda")
+    ms = plan.execute_device_timed(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
+    assert len(ms) == d["num_launches"] and all(m > 0 for m in ms)
+    assert d["launch_kind"][0] == "tree" and d["launch_kind"][-1] == "interleave"
+
+
+def test_device_errors():
+    plan = pifft.Plan(64, 2, 1, pifft.F64)
+    x = torch.zeros(64, dtype=torch.complex128, device="cuda")
+    with pytest.raises(pifft.PifftError, match="in-place"):
+        plan.execute_device(x.data_ptr(), x.data_ptr())
+    with pytest.raises(pifft.PifftError, match="device"):
+        pifft.Plan(64, 2, 1, pifft.F64, first=0, count=2, device=pifft.gpu_count())
+
+
+# ------------------------------------------------------ full-size properties ---
+def _dft_bins(x, ks):
+    """Direct DFT bins in float64 (chunked; exact integer phase)."""
+    n = len(x)
+    out = []
+    for k in ks:
+        acc = 0j
+        for s in range(0, n, 1 << 22):
+            idx = np.arange(s, min(n, s + (1 << 22)), dtype=np.int64)
+            ph = (idx * k) % n
+            acc += np.sum(x[s:s + len(idx)].astype(np.complex128) * np.exp(-2j * np.pi * ph / n))
+        out.append(acc)
+    return np.array(out)
+
+
+@pytest.mark.parametrize("logn,P", [(24, 1), (24, 8), (26, 4), (28, 1), (28, 8)])
+def test_large_fp64_properties(logn, P):
+    n = 1 << logn
+    x = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=torch.cuda.current_stream())
+    plan = pifft.Plan(n, P, 1, pifft.F64)
+    X = torch.empty_like(x)
+    plan.execute_device(x.data_ptr(), X.data_ptr(), torch.cuda.current_stream())
+    # double transform: FFT(conj(FFT(x))) = N conj(x)
+    Y = torch.empty_like(x)
+    Xc = X.conj().resolve_conj().contiguous()
+    plan.execute_device(Xc.data_ptr(), Y.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    err = (torch.linalg.vector_norm(Y.conj() / n - x) / torch.linalg.vector_norm(x)).item()
+    assert err <= 1e-12, err
+    # Parseval
+    pe = abs(torch.linalg.vector_norm(X).item() ** 2 / n - torch.linalg.vector_norm(x).item() ** 2)
+    assert pe <= 1e-12 * torch.linalg.vector_norm(x).item() ** 2
+    # direct DFT bins
+    xh = x.cpu().numpy()
+    ks = [0, 1, n // 2 + 3, n - 1, 12345 % n]
+    want = _dft_bins(xh, ks)
+    got = X.cpu().numpy()[ks]
+    scale = np.linalg.norm(xh)  # |X[k]| ~ ||x||
+    assert np.max(np.abs(got - want)) <= 1e-12 * scale * math.sqrt(n) * 10
+    del Y, Xc
+    if logn <= 24:  # the oracle itself (8 threads) at 2^24
+        want_full = oracle.fft(xh, P=8, nthreads=8)
+        assert_bins_close(X.cpu().numpy(), want_full, "f64", n)
+
+
+def test_large_split_consistency_fp64():
+    """2^28 split over 8 single-worker plans (the 8-GPU job, one GPU at a time)
+    equals the 1-worker transform bin for bin."""
+    n, P = 1 << 28, 8
+    x = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=torch.cuda.current_stream())
+    full = torch.empty_like(x)
+    pifft.Plan(n, 1, 1, pifft.F64).execute_device(x.data_ptr(), full.data_ptr(), torch.cuda.current_stream())
+    for q in (0, 3, 7):
+        plan = pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0)
+        s = torch.empty(n // P, dtype=torch.complex128, device="cuda")
+        plan.execute_device(x.data_ptr(), s.data_ptr(), torch.cuda.current_stream())
+        r = pifft_dist.bitrev(q, 3)
+        ref = full[r::P]
+        torch.cuda.synchronize()
+        err = (torch.linalg.vector_norm(s - ref) / torch.linalg.vector_norm(ref)).item()
+        assert err <= 1e-12, (q, err)
+
+
+def test_large_fp64_linearity():
+    n = 1 << 26
+    a = torch.empty(n, dtype=torch.complex128, device="cuda")
+    b = torch.empty_like(a)
+    pifft.generate_device(a.data_ptr(), n, n, pifft.F64, seed=1, stream=torch.cuda.current_stream())
+    pifft.generate_device(b.data_ptr(), n, n, pifft.F64, seed=2, stream=torch.cuda.current_stream())
+    plan = pifft.Plan(n, 1, 1, pifft.F64)
+    outs = []
+    for v in (a, b, (2.0 * a - 3.0 * b).contiguous()):
+        o = torch.empty_like(v)
+        plan.execute_device(v.data_ptr(), o.data_ptr(), torch.cuda.current_stream())
+        outs.append(o)
+    torch.cuda.synchronize()
+    lhs, rhs = outs[2], 2.0 * outs[0] - 3.0 * outs[1]
+    assert (torch.linalg.vector_norm(lhs - rhs) / torch.linalg.vector_norm(rhs)).item() <= 1e-13
+
+
+# -------------------------------------------------------------------- CLI ---
+def _cli(args):
+    import subprocess
+    return subprocess.run([pifft.CLI_PATH] + args, capture_output=True, text=True, timeout=300)
+
+
+@pytest.mark.parametrize("prec", ["32", "64"])
+@pytest.mark.parametrize("P", ["1", "2", "4", "8"])
+def test_cli_known_answer(prec, P):
+    r = _cli(["-t", "-p", P, "-f", prec])
+    assert r.returncode == 0, r.stderr
+    assert "Output is correct. Test passed." in r.stdout
+    assert "4.0+0.0i, 0.0+0.0i, 0.0+0.0i, 0.0+0.0i, -4.0+0.0i" in r.stdout
+
+
+def test_cli_tsv_and_dump(tmp_path):
+    r = _cli(["-n", "65536", "-p", "8", "-o"])
+    assert r.returncode == 0, r.stderr
+    cols = r.stdout.strip().split("\t")
+    assert len(cols) == 5 and cols[0] == "65536" and cols[1] == "8"
+    assert abs(float(cols[2]) - float(cols[3]) - float(cols[4])) < 1e-3
+    r = _cli(["-n", "1024", "-p", "4"])
+    assert r.stdout.splitlines()[0] == "n\tp\ttime (total)\ttime (stage 1)\ttime (stage 2)"
+    out = tmp_path / "x.bin"
+    r = _cli(["-n", "4096", "-p", "4", "-f", "64", "-s", "7", "-w", str(out), "-o"])
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.complex128)
+    x = oracle.generate(4096, np.complex128, seed=7)
+    assert_bins_close(got, oracle.fft(x, P=4), "f64", 4096)
