@@ -123,8 +123,6 @@ struct Step {
     uint64_t src_off = 0, dst_off = 0;  // elements
     PassArgs pa{};
     TreeArgs ta{};
-    TreeStageArgs tsa{};
-    int tree_kind = 0;  // 1 fused network, 2 staged level
     uint64_t il_total = 0;
     uint32_t il_log_n = 0, il_log_p = 0;
     uint64_t bytes = 0;
@@ -322,66 +320,48 @@ int build_plan(pifft_plan* p) {
     const uint64_t M = p->m;
     if (need_tree) {
         Elem e;
-        if (p->lp <= 4) {
+        // ceil(log2 P / 4) launches of up to 4 levels each; in place over
+        // one position-space buffer between launches (see k_tree)
+        static const void* tk64[5] = {nullptr, (const void*)&k_tree<double, 1>, (const void*)&k_tree<double, 2>,
+                                      (const void*)&k_tree<double, 3>, (const void*)&k_tree<double, 4>};
+        static const void* tk32[5] = {nullptr, (const void*)&k_tree<float, 1>, (const void*)&k_tree<float, 2>,
+                                      (const void*)&k_tree<float, 3>, (const void*)&k_tree<float, 4>};
+        const int nl = (p->lp + 3) / 4;
+        // number of level-t blocks (P >> t workers each) holding a requested worker
+        auto blocks_needed = [&](int t) -> uint64_t {
+            const uint64_t w = (uint64_t)p->P >> t;
+            return ((uint64_t)p->q0 + p->nq - 1) / w - (uint64_t)p->q0 / w + 1;
+        };
+        int t0 = 0;
+        for (int l = 0; l < nl; l++) {
+            const int L = (p->lp - t0 + (nl - l) - 1) / (nl - l);  // spread levels evenly
+            const bool first = (l == 0), last = (l == nl - 1);
             Step s;
             s.kind = STEP_TREE;
-            s.tree_kind = 1;
-            const bool d = p->prec == 64;
-            static const void* tk64[5] = {nullptr, (const void*)&k_tree<double, 1>, (const void*)&k_tree<double, 2>,
-                                          (const void*)&k_tree<double, 3>, (const void*)&k_tree<double, 4>};
-            static const void* tk32[5] = {nullptr, (const void*)&k_tree<float, 1>, (const void*)&k_tree<float, 2>,
-                                          (const void*)&k_tree<float, 3>, (const void*)&k_tree<float, 4>};
-            s.fn = d ? tk64[p->lp] : tk32[p->lp];
+            s.fn = p->prec == 64 ? tk64[L] : tk32[L];
+            s.src = first ? -1 : BUF_TA;  // -1: chain input
+            s.dst = last ? -2 : BUF_TA;   // -2: chain output (slice-major)
             s.ta.tw_direct = tree_is_direct ? twp(tree_direct) : nullptr;
             s.ta.tw_lo = tree_is_direct ? nullptr : twp(tree2.lo);
             s.ta.tw_hi = tree_is_direct ? nullptr : twp(tree2.hi);
             s.ta.tw_h = tree2.h;
             s.ta.in_bstride = p->n;
-            s.ta.out_bstride = (uint64_t)p->nq * M;
-            s.ta.total = (uint64_t)p->batch * M;
-            s.ta.log_m = (uint32_t)p->log_m;
+            s.ta.out_bstride = last ? (uint64_t)p->nq * M : p->n;
+            s.ta.out_shift = last ? -(int64_t)((uint64_t)p->q0 * M) : 0;
+            s.ta.total = (uint64_t)p->batch * (p->n >> L);
+            s.ta.log_n = (uint32_t)p->log_n;
+            s.ta.log_p = (uint32_t)p->lp;
+            s.ta.t0 = (uint32_t)t0;
             s.ta.q0 = p->q0;
             s.ta.nq = p->nq;
             s.block = dim3(256);
             s.grid = dim3((unsigned)((s.ta.total + 255) / 256));
-            s.bytes = (uint64_t)p->batch * (p->n + (uint64_t)p->nq * M) * esz;
+            s.bytes = (uint64_t)p->batch * esz *
+                      (blocks_needed(t0) * (p->n >> t0) + blocks_needed(t0 + L) * (p->n >> (t0 + L)));
             e.steps.push_back(s);
-        } else {
-            // staged: per worker, one launch per radix-2 level (compact blocks)
-            p->bytes_ta = (size_t)p->batch * (p->n / 2) * esz;
-            p->bytes_tb = (size_t)p->batch * ((p->n / 4) ? p->n / 4 : 1) * esz;
-            const void* fn = p->prec == 64 ? (const void*)&k_tree_stage<double> : (const void*)&k_tree_stage<float>;
-            for (uint32_t q = p->q0; q < p->q0 + p->nq; q++) {
-                uint64_t size = p->n;
-                for (int t = 0; t < p->lp; t++, size /= 2) {
-                    Step s;
-                    s.kind = STEP_TREE;
-                    s.tree_kind = 2;
-                    s.fn = fn;
-                    const int iter = p->lp - t;                       // CPU.c:419
-                    const bool left = ((q >> (iter - 1)) % 2 == 0);  // CPU.c:429
-                    const bool lastlvl = (t == p->lp - 1);
-                    s.src = (t == 0) ? -1 : ((t % 2 == 1) ? BUF_TA : BUF_TB);  // -1: chain input
-                    s.dst = lastlvl ? -2 : ((t % 2 == 0) ? BUF_TA : BUF_TB);   // -2: chain output
-                    s.dst_off = lastlvl ? (uint64_t)(q - p->q0) * M : 0;
-                    s.tsa.tw_direct = tree_is_direct ? twp(tree_direct) : nullptr;
-                    s.tsa.tw_lo = tree_is_direct ? nullptr : twp(tree2.lo);
-                    s.tsa.tw_hi = tree_is_direct ? nullptr : twp(tree2.hi);
-                    s.tsa.tw_h = tree2.h;
-                    s.tsa.in_bstride = (t == 0) ? p->n : size;
-                    s.tsa.out_bstride = lastlvl ? (uint64_t)p->nq * M : size / 2;
-                    s.tsa.half = size / 2;
-                    s.tsa.log_half = (uint32_t)ilog2u(size / 2);
-                    s.tsa.total = (uint64_t)p->batch * (size / 2);
-                    s.tsa.t = (uint32_t)t;
-                    s.tsa.right = left ? 0u : 1u;
-                    s.block = dim3(256);
-                    s.grid = dim3((unsigned)((s.tsa.total + 255) / 256));
-                    s.bytes = (uint64_t)p->batch * (size + size / 2) * esz;
-                    e.steps.push_back(s);
-                }
-            }
+            t0 += L;
         }
+        if (nl > 1) p->bytes_ta = (size_t)p->batch * p->n * esz;
         p->tree_steps = (int)e.steps.size();
         chain.push_back(e);
     }
@@ -441,7 +421,7 @@ int build_plan(pifft_plan* p) {
         const int src = (i == 0) ? BUF_IN : dst[i - 1];
         if (dst[i] == BUF_W || src == BUF_W) need_w = true;
         for (auto& s : chain[i].steps) {
-            if (s.kind == STEP_TREE && s.tree_kind == 2) {
+            if (s.kind == STEP_TREE) {
                 if (s.src == -1) s.src = src;
                 if (s.dst == -2) s.dst = dst[i];
             } else {
@@ -520,19 +500,11 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             break;
         }
         case STEP_TREE: {
-            if (s.tree_kind == 1) {
-                TreeArgs a = s.ta;
-                a.in = src;
-                a.out = dst;
-                void* args[] = {&a};
-                e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
-            } else {
-                TreeStageArgs a = s.tsa;
-                a.in = src;
-                a.out = dst;
-                void* args[] = {&a};
-                e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
-            }
+            TreeArgs a = s.ta;
+            a.in = src;
+            a.out = dst;
+            void* args[] = {&a};
+            e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
             break;
         }
         case STEP_INTERLEAVE: {
@@ -798,8 +770,8 @@ int pifft_tree_device(pifft_plan* p, const void* d_in, void* d_seg, void* stream
     }
     for (int i = 0; i < p->tree_steps; i++) {
         Step s = p->steps[i];
-        if (s.tree_kind == 1 || (s.dst != BUF_TA && s.dst != BUF_TB)) s.dst = BUF_OUT;
-        if (s.tree_kind == 1 || (s.src != BUF_TA && s.src != BUF_TB)) s.src = BUF_IN;
+        if (s.dst != BUF_TA) s.dst = BUF_OUT;
+        if (s.src != BUF_TA) s.src = BUF_IN;
         if (launch_step(p, s, d_in, d_seg, st)) return -1;
     }
     return 0;

@@ -15,7 +15,8 @@
 //               the requested workers.  With the host-built omega(N,k) table
 //               (CPU.c:644-651 formula) its output is bit-identical to the
 //               reference's post-tree segment.
-//  * k_tree_stage -- the same stage one radix-2 level per launch, for P > 16.
+//               Up to 4 levels per launch; log2 P > 4 takes ceil(log2 P / 4)
+//               launches, in place over the reference's scratch layout.
 //  * k_pass   -- one Stockham pass of the local N/P-point FFT: each workgroup
 //               stages C adjacent "lines" (sub-FFTs of length R, elements
 //               strided by M/R in HBM) in LDS, applies the inter-pass twiddle,
@@ -306,6 +307,14 @@ __global__ __launch_bounds__((PassCfg<R, C>::NT)) void k_pass(PassArgs a) {
 // ---------------------------------------------------------------------------
 // Tree ("funnel") stage
 // ---------------------------------------------------------------------------
+// Levels t0 .. t0+L-1 of the reference's radix-2 tree (CPU.c:419-448, level t
+// = butterflies of size N >> t) in "position space": the reference's scratch
+// layout, where after all log2 P levels worker q's segment sits at
+// [q N/P, (q+1) N/P).  A thread owns 2^L positions base + i + m*D
+// (D = N >> (t0+L)), which only interact with each other in these levels, so
+// one launch applies L levels in registers and writes the same positions back
+// (in place).  Only branches leading to workers [q0, q0+nq) are evaluated and
+// stored; the last launch writes slice-major (out_shift = -q0 N/P).
 struct TreeArgs {
     const void* in;
     void* out;
@@ -313,9 +322,10 @@ struct TreeArgs {
     const void* tw_lo;      // else two-level w_N
     const void* tw_hi;
     uint64_t in_bstride;    // N
-    uint64_t out_bstride;   // count * M
-    uint64_t total;         // transforms * M
-    uint32_t log_m;         // log2(N/P)
+    uint64_t out_bstride;   // N (position space) or nq * N/P (slice-major)
+    int64_t out_shift;      // 0 or -q0 * N/P
+    uint64_t total;         // transforms * (N >> L)
+    uint32_t log_n, log_p, t0;
     uint32_t tw_h;
     uint32_t q0, nq;        // workers [q0, q0+nq)
 };
@@ -326,82 +336,55 @@ __device__ __forceinline__ cx<T> tree_tw(const TreeArgs& a, uint64_t e) {
     return tw2(static_cast<const cx<T>*>(a.tw_lo), static_cast<const cx<T>*>(a.tw_hi), a.tw_h, e);
 }
 
-template <typename T, int LP>
+template <typename T, int L>
 __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
     using C2 = cx<T>;
-    constexpr int P = 1 << LP;
+    constexpr int V = 1 << L;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.total) return;
-    const uint64_t M = 1ull << a.log_m;
-    const uint64_t i = gid & (M - 1), bt = gid >> a.log_m;
-    const C2* __restrict__ src = static_cast<const C2*>(a.in) + bt * a.in_bstride + i;
-    C2 v[P];
+    const uint32_t log_g = a.log_n - L;            // threads per transform = 2^log_g
+    const uint32_t log_d = a.log_n - a.t0 - L;     // D = stride between a thread's positions
+    const uint64_t g = gid & ((1ull << log_g) - 1), bt = gid >> log_g;
+    const uint64_t blk0 = g >> log_d, i = g & ((1ull << log_d) - 1);
+    const uint64_t base = blk0 << (a.log_n - a.t0);
+    // v[m] ends in the level-(t0+L) block (blk0 << L) + m, which leads to
+    // workers [((blk0 << L) + m) W, +W), W = P >> (t0 + L)
+    const uint32_t log_w = a.log_p - a.t0 - L;
+    const uint64_t q0 = a.q0, q1 = (uint64_t)a.q0 + a.nq;
+    const uint64_t w_lo = (blk0 << L) << log_w, w_hi = ((blk0 + 1) << L) << log_w;
+    if (w_hi <= q0 || w_lo >= q1) return;  // no requested worker below this group
+    const C2* __restrict__ src = static_cast<const C2*>(a.in) + bt * a.in_bstride + base + i;
+    C2 v[V];
 #pragma unroll
-    for (int m = 0; m < P; m++) v[m] = src[(uint64_t)m << a.log_m];
-    const int q0 = (int)a.q0, q1 = (int)(a.q0 + a.nq);
-    // stage t (block size N >> t): CPU.c:419-448, one level of the radix-2 tree
+    for (int m = 0; m < V; m++) v[m] = src[(uint64_t)m << log_d];
 #pragma unroll
-    for (int t = 0; t < LP; t++) {
-        const int BS = P >> t, H = BS >> 1;
+    for (int tl = 0; tl < L; tl++) {
+        const int BS = V >> tl, H = BS >> 1;
+        const uint32_t t = a.t0 + tl;  // global level: butterfly size N >> t
 #pragma unroll
-        for (int blk = 0; blk < (1 << t); blk++) {
+        for (int blk = 0; blk < (1 << tl); blk++) {
             const int lo = blk * BS;
-            // children [lo, lo+H) and [lo+H, lo+BS) of v-indices == worker ids below
-            const bool needL = (lo < q1) && (lo + H > q0);
-            const bool needR = (lo + H < q1) && (lo + BS > q0);
+            const uint64_t cl0 = (((blk0 << L) + lo) << log_w), cl1 = (((blk0 << L) + lo + H) << log_w);
+            const uint64_t cr1 = (((blk0 << L) + lo + BS) << log_w);
+            const bool needL = (cl0 < q1) && (cl1 > q0);
+            const bool needR = (cl1 < q1) && (cr1 > q0);
 #pragma unroll
             for (int ml = 0; ml < H; ml++) {
                 const C2 x0 = v[lo + ml], x1 = v[lo + ml + H];
-                if (needL) v[lo + ml] = cadd(x0, x1);                        // butterfly_left
-                if (needR) {                                                 // butterfly_right
-                    const uint64_t e = (i + ((uint64_t)ml << a.log_m)) << t;  // b * N/size
+                if (needL) v[lo + ml] = cadd(x0, x1);                         // butterfly_left
+                if (needR) {                                                  // butterfly_right
+                    const uint64_t e = (i + ((uint64_t)ml << log_d)) << t;    // b * N/size
                     v[lo + ml + H] = cmul(csub(x0, x1), tree_tw<T>(a, e));
                 }
             }
         }
     }
-    C2* __restrict__ dst = static_cast<C2*>(a.out) + bt * a.out_bstride + i;
+    C2* __restrict__ dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (int64_t)(base + i) + a.out_shift;
 #pragma unroll
-    for (int q = 0; q < P; q++)
-        if (q >= q0 && q < q1) dst[(uint64_t)(q - q0) << a.log_m] = v[q];
-}
-
-// One radix-2 level of the tree for one worker (P > 16): compact block in,
-// compact half out (the reference's loop body, CPU.c:432-443, in parallel).
-struct TreeStageArgs {
-    const void* in;
-    void* out;
-    const void* tw_direct;
-    const void* tw_lo;
-    const void* tw_hi;
-    uint64_t in_bstride, out_bstride;
-    uint64_t half;   // size/2
-    uint64_t total;  // transforms * half
-    uint32_t log_half;
-    uint32_t t;      // level: twiddle exponent b << t
-    uint32_t right;
-    uint32_t tw_h;
-};
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_tree_stage(TreeStageArgs a) {
-    using C2 = cx<T>;
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= a.total) return;
-    const uint64_t b = gid & (a.half - 1), bt = gid >> a.log_half;
-    const C2* src = static_cast<const C2*>(a.in) + bt * a.in_bstride;
-    const C2 x0 = src[b], x1 = src[b + a.half];
-    C2 r;
-    if (a.right) {
-        const uint64_t e = b << a.t;
-        C2 w;
-        if (a.tw_direct) w = static_cast<const C2*>(a.tw_direct)[e];
-        else w = tw2(static_cast<const C2*>(a.tw_lo), static_cast<const C2*>(a.tw_hi), a.tw_h, e);
-        r = cmul(csub(x0, x1), w);
-    } else {
-        r = cadd(x0, x1);
+    for (int m = 0; m < V; m++) {
+        const uint64_t wm = ((blk0 << L) + m) << log_w;
+        if (wm < q1 && wm + (1ull << log_w) > q0) dst[(uint64_t)m << log_d] = v[m];
     }
-    static_cast<C2*>(a.out)[bt * a.out_bstride + b] = r;
 }
 
 // ---------------------------------------------------------------------------
