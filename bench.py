@@ -184,7 +184,7 @@ def main() -> None:
     for i in range(nl):
         kind = desc["launch_kind"][i] if i < len(desc["launch_kind"]) else "?"
         b = desc["launch_bytes"][i] if i < len(desc["launch_bytes"]) else 0
-        launches.append({"kind": kind, "ms": round(avg[i], 4),
+        launches.append({"kind": kind, "bytes": b, "ms": round(avg[i], 4),
                          "GB/s": round(b / (avg[i] * 1e-3) / 1e9, 1) if avg[i] > 0 else None})
     total_bytes = sum(desc["launch_bytes"][:nl])
 

@@ -641,7 +641,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
 int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* stream) {
     if (check_buffers(p, d_in, d_out)) return -1;
     DeviceGuard g(p->device);
-    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
     for (const auto& s : p->steps)
         if (launch_step(p, s, d_in, d_out, st)) return -1;
     return 0;
@@ -651,7 +651,7 @@ int pifft_execute_device_timed(pifft_plan* p, const void* d_in, void* d_out, voi
                                float* launch_ms, int max_launches) {
     if (check_buffers(p, d_in, d_out)) return -1;
     DeviceGuard g(p->device);
-    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
     std::vector<float> ms;
     if (run_timed(p, d_in, d_out, st, ms)) return -1;
     if (launch_ms)
@@ -763,7 +763,7 @@ int pifft_interleave_device(const void* d_slices, void* d_out, uint64_t n, uint3
 int pifft_tree_device(pifft_plan* p, const void* d_in, void* d_seg, void* stream) {
     if (check_buffers(p, d_in, d_seg)) return -1;
     DeviceGuard g(p->device);
-    hipStream_t st = stream ? (hipStream_t)stream : p->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
     if (p->tree_steps == 0) {  // P == 1: the segment is the input
         HIPCHK(hipMemcpyAsync(d_seg, d_in, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToDevice, st));
         return 0;

@@ -98,7 +98,7 @@ int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
 
 /* Device boundary: d_in holds info.in_elems complex values, d_out receives
  * info.out_elems (d_in != d_out; neither is freed).  Asynchronous on `stream`
- * (a hipStream_t, NULL = the plan's own stream). */
+ * (a hipStream_t; NULL = the default stream, as in other ROCm libraries). */
 int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* stream);
 
 /* As pifft_execute_device, but records a HIP event before every launch and

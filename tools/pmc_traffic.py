@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""tools/pmc_traffic.py -- HBM traffic per launch from rocprofv3 PMC counters.
+
+Recipe (MI355X_MICROARCH.md, HBM / rocprofv3 PMC slots):
+  * FETCH_SIZE and WRITE_SIZE (units: KiB) do not fit in one TCC pass, so each
+    is collected in its own `rocprofv3 --pmc` run (no tracing options beside
+    --pmc);
+  * gfx950 correction: FETCH_SIZE reports exactly half of the bytes of a wide
+    (16 B/lane) coalesced streaming read -> x2 for the fp64 kernels here;
+    WRITE_SIZE is exact for 16 B/lane streaming stores.  (8 B/lane fp32
+    accesses are uncalibrated: reported uncorrected, flagged.)
+
+Runs bench.py under each counter pass, maps the timed loop's dispatches to
+the plan's launch indices (the plan's launches repeat in order every step),
+and writes profiles/<tag>_traffic.json, which bench.py reads for
+roofline.traffic.
+
+usage: python tools/pmc_traffic.py --tag r01 [bench.py args...]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OURS = ("k_pass", "k_tree", "k_interleave")
+
+
+def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[dict], dict]:
+    """rocprofv3 --pmc <counter> -- python bench.py ...; returns (rows, bench JSON line).
+    This process never touches the GPU (rocprofv3 and bench.py are children)."""
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
+           sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
+    r = subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in r.stdout.splitlines():
+        if ln.startswith("{") and '"metric"' in ln:
+            line = json.loads(ln)
+    if line is None:
+        raise SystemExit("bench.py printed no JSON line")
+    files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {outdir}")
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            rows += list(csv.DictReader(fh))
+    return rows, line
+
+
+def per_dispatch(rows: list[dict], counter: str) -> list[tuple[int, str, float]]:
+    acc: dict[int, list] = {}
+    for r in rows:
+        if r.get("Counter_Name") != counter:
+            continue
+        did = int(r.get("Dispatch_Id", r.get("Correlation_Id", 0)))
+        name = r.get("Kernel_Name", "")
+        v = float(r.get("Counter_Value", 0.0))
+        if did in acc:
+            acc[did][1] += v
+        else:
+            acc[did] = [name, v]
+    return [(d, acc[d][0], acc[d][1]) for d in sorted(acc)]
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--outdir", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    args, rest = ap.parse_known_args()
+    bench_args = ["--steps", str(args.steps), "--warmup", "1", "--no-cpu-baseline"] + rest
+
+    ba = argparse.ArgumentParser()
+    ba.add_argument("--prec", type=int, default=64)
+    b, _ = ba.parse_known_args(rest)
+    result = {"counters": {}, "kernels": {}}
+    per_launch = defaultdict(dict)
+    line = None
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows, line = run_pass(counter, os.path.join(args.outdir, counter.lower()), bench_args)
+        launches = line["config"]["launches"]
+        nl = len(launches)
+        disp = [d for d in per_dispatch(rows, counter) if any(o in d[1] for o in OURS)]
+        timed = disp[-args.steps * nl:]
+        for i in range(nl):
+            vals = [timed[s * nl + i][2] for s in range(args.steps) if s * nl + i < len(timed)]
+            per_launch[i][counter] = sum(vals) / max(len(vals), 1)
+            per_launch[i]["kernel"] = timed[i][1] if i < len(timed) else "?"
+        result["counters"][counter] = len(disp)
+    cfg = line["config"]
+    key = f"n2^{cfg['n'].bit_length() - 1}_f{b.prec}_b{cfg['batch']}_P{cfg['workers']}_q{cfg['workers_per_gpu']}"
+    result["config_key"] = key
+    nl = len(cfg["launches"])
+    launch_bytes = [l.get("bytes") for l in cfg["launches"]]
+    wide = b.prec == 64
+    out = {}
+    for i in range(nl):
+        f_kib = per_launch[i].get("FETCH_SIZE", 0.0)
+        w_kib = per_launch[i].get("WRITE_SIZE", 0.0)
+        fetch = f_kib * 1024 * (2 if wide else 1)
+        write = w_kib * 1024
+        out[str(i)] = fetch + write
+        result["kernels"][str(i)] = {"kernel": per_launch[i]["kernel"], "FETCH_SIZE_KiB": f_kib,
+                                     "WRITE_SIZE_KiB": w_kib, "fetch_bytes_corrected": fetch,
+                                     "write_bytes": write, "algorithmic_bytes": launch_bytes[i]}
+    result["per_launch_bytes"] = out
+    result["correction"] = ("FETCH_SIZE KiB x1024 x2 (gfx950 16 B/lane streaming read), WRITE_SIZE KiB x1024"
+                            if wide else "uncorrected (8 B/lane accesses uncalibrated)")
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    path = os.path.join(ROOT, "profiles", f"{args.tag}_traffic_{key}.json")
+    with open(path, "w") as f:
+        json.dump(result, f, indent=1)
+    print(json.dumps(result, indent=1))
+
+
+if __name__ == "__main__":
+    main()
