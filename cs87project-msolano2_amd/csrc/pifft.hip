@@ -66,47 +66,28 @@ uint32_t bitrev(uint32_t x, int m) { return m ? (__builtin_bitreverse32(x) >> (3
 // pass kernel instantiations
 // ---------------------------------------------------------------------------
 struct PassKernel {
-    int prec, R, C;
+    int prec, R, C, mode;
     const void* fn;
     int nt;
     int lds_bytes;
 };
 
-#define PK(T, PREC, R, C)                                                       \
+#define PK(T, PREC, R, C, MODE)                                                 \
     PassKernel {                                                                \
-        PREC, R, C, reinterpret_cast<const void*>(&k_pass<T, R, C>),            \
-            PassCfg<R, C>::NT, PassCfg<R, C>::lds_elems * (int)sizeof(cx<T>)    \
+        PREC, R, C, MODE, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE>),\
+            PassCfg<R, C>::NT, PassCfg<R, C>::lds_elems * (int)sizeof(T)        \
     }
-#define PK_C5(T, PREC, R) PK(T, PREC, R, 1), PK(T, PREC, R, 2), PK(T, PREC, R, 4), PK(T, PREC, R, 8), PK(T, PREC, R, 16)
-#define PK_C4(T, PREC, R) PK(T, PREC, R, 1), PK(T, PREC, R, 2), PK(T, PREC, R, 4), PK(T, PREC, R, 8)
 
 const PassKernel g_pass_kernels[] = {
-    // fp64 (16 B / element): LDS <= 160 KiB, <= 1024 threads
-    PK(double, 64, 2, 64), PK(double, 64, 4, 64), PK(double, 64, 8, 64),
-    PK_C5(double, 64, 16), PK_C5(double, 64, 32), PK_C5(double, 64, 64), PK_C5(double, 64, 128),
-    PK_C5(double, 64, 256), PK_C5(double, 64, 512), PK_C4(double, 64, 1024),
-    PK(double, 64, 2048, 1), PK(double, 64, 2048, 2), PK(double, 64, 2048, 4),
-    PK(double, 64, 4096, 1), PK(double, 64, 4096, 2), PK(double, 64, 8192, 1),
-    // fp32 (8 B / element)
-    PK(float, 32, 2, 64), PK(float, 32, 4, 64), PK(float, 32, 8, 64),
-    PK_C5(float, 32, 16), PK_C5(float, 32, 32), PK_C5(float, 32, 64), PK_C5(float, 32, 128),
-    PK_C5(float, 32, 256), PK_C5(float, 32, 512), PK_C5(float, 32, 1024), PK_C4(float, 32, 2048),
-    PK(float, 32, 4096, 1), PK(float, 32, 4096, 2), PK(float, 32, 4096, 4),
-    PK(float, 32, 8192, 1), PK(float, 32, 8192, 2), PK(float, 32, 16384, 1),
+#include "pifft_instances.inc"
 };
 
-const PassKernel* find_pass(int prec, int R, int C) {
+const PassKernel* find_pass(int prec, int R, int C, int mode) {
     for (const auto& k : g_pass_kernels)
-        if (k.prec == prec && k.R == R && k.C == C) return &k;
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode) return &k;
     return nullptr;
 }
 
-int max_lines(int prec, int R) {
-    int best = 0;
-    for (const auto& k : g_pass_kernels)
-        if (k.prec == prec && k.R == R && k.C > best) best = k.C;
-    return best;
-}
 
 // ---------------------------------------------------------------------------
 // plan
@@ -224,41 +205,51 @@ struct PassChoice {
     int R, C;
 };
 
+// Tile = R x C elements per workgroup (C adjacent lines of an R-point sub-FFT).
+// Default tile 8192 (fp64) / 16384 (fp32): 128 KiB of data in registers, one
+// component (64 KiB) in LDS at a time -> two workgroups per CU; at R = 512 the
+// lines give 256-B contiguous row segments (the HBM-efficient width measured
+// by tools/probe_bw.hip).
+int tile_elems(int prec) {
+    return env_int(prec == 64 ? "PIFFT_TILE64" : "PIFFT_TILE32", prec == 64 ? 8192 : 16384);
+}
+
+int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, const char* env_c, int mode) {
+    int C = env_int(env_c, 0);
+    // single pass: lines are whole contiguous transforms, no segment-width
+    // constraint -> small tiles (measured best: C = 4096/R, i.e. C=1 at 4096)
+    const int tile = mode == 0 ? env_int(prec == 64 ? "PIFFT_SINGLE_TILE64" : "PIFFT_SINGLE_TILE32", 4096)
+                               : tile_elems(prec);
+    if (C <= 0) C = tile / R;
+    if (C < 1) C = 1;
+    if (C > 64) C = 64;
+    if (R <= 8) C = 64;
+    while (C > 1 && (uint64_t)C > ntrans_lines_cap && R > 8) C /= 2;
+    while (C > 1 && !find_pass(prec, R, C, mode)) C /= 2;
+    return C;
+}
+
 int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
-    const int single_max = env_int("PIFFT_SINGLE_MAX_LOG", prec == 64 ? 13 : 14);
+    const int single_max = env_int("PIFFT_SINGLE_MAX_LOG", 14);
     if (logm <= single_max) {
         const int R = (int)M;
-        int C;
-        if (R <= 8) {
-            C = 64;
-        } else {
-            const int target = env_int(prec == 64 ? "PIFFT_SINGLE_ELEMS64" : "PIFFT_SINGLE_ELEMS32",
-                                       prec == 64 ? 4096 : 8192);
-            C = target / R;
-            if (C < 1) C = 1;
-            if (C > 16) C = 16;
-            while (C > 1 && (uint64_t)(C / 2) >= ntrans) C /= 2;
-            const int mx = max_lines(prec, R);
-            if (C > mx) C = mx;
-        }
+        const int C = pick_lines(prec, R, ntrans, prec == 64 ? "PIFFT_SINGLE_C64" : "PIFFT_SINGLE_C32", 0);
+        if (!find_pass(prec, R, C, 0)) return fail("no pass kernel for R=%d C=%d", R, C);
         out.push_back({R, C});
         return 0;
     }
-    const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32",
-                                 prec == 64 ? 10 : 11);
+    const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32", 10);
     const int k = (logm + rmax_log - 1) / rmax_log;
     const int base = logm / k, extra = logm % k;
     for (int p = 0; p < k; p++) {
         const int bits = base + (p < extra ? 1 : 0);
         const int R = 1 << bits;
-        int C = env_int(prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", prec == 64 ? 8 : 16);
-        const int mx = max_lines(prec, R);
-        if (C > mx) C = mx;
-        if ((uint64_t)C > (M >> bits)) C = (int)(M >> bits);
-        if (!find_pass(prec, R, C)) return fail("no pass kernel for R=%d C=%d", R, C);
+        const int mode = p == 0 ? 1 : 2;
+        const int C = pick_lines(prec, R, M >> bits, prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
+        if (!find_pass(prec, R, C, mode)) return fail("no pass kernel for R=%d C=%d mode %d", R, C, mode);
         out.push_back({R, C});
     }
     return 0;
@@ -368,7 +359,8 @@ int build_plan(pifft_plan* p) {
     uint64_t ns = 1;
     p->npasses = (int)passes.size();
     for (size_t i = 0; i < passes.size(); i++) {
-        const PassKernel* k = find_pass(p->prec, passes[i].R, passes[i].C);
+        const int mode = passes.size() == 1 ? 0 : (i == 0 ? 1 : 2);
+        const PassKernel* k = find_pass(p->prec, passes[i].R, passes[i].C, mode);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = STEP_PASS;

@@ -158,6 +158,15 @@ __device__ __forceinline__ cx<T> tw2(const cx<T>* __restrict__ lo, const cx<T>* 
 // ---------------------------------------------------------------------------
 // Stockham pass
 // ---------------------------------------------------------------------------
+// One pass of the local FFT (Stockham auto-sort, natural order in and out):
+// for each line j < M/R of each transform, v_r = in[j + r M/R] (r < R),
+// v_r *= w_{Ns R}^{(j mod Ns) r}, V = DFT_R(v),
+// out[(j/Ns) Ns R + (j mod Ns) + r' Ns] = V_r'.
+// A workgroup owns C adjacent lines (C*16 B contiguous per row on both sides
+// for fp64) and keeps them in registers, 16 values per thread; the R-point
+// DFT is one radix-2/4/8/16 stage plus radix-16 stages, with the values
+// exchanged through LDS between stages one component at a time (re, then im),
+// so the LDS footprint is C*R*sizeof(T) and two workgroups fit per CU.
 struct PassArgs {
     const void* in;
     void* out;
@@ -175,133 +184,191 @@ struct PassArgs {
 
 template <int R>
 struct PassShape {
-    static constexpr int Q = R >= 16 ? 16 : R;             // radix of the wide stages
+    static constexpr int Q = R >= 16 ? 16 : R;              // values per thread
     static constexpr int LOGR = ilog2c(R);
-    static constexpr int NSTG = (LOGR + 3) / 4;             // radix-16 stages + 1 leading
-    static constexpr int Q0 = 1 << (LOGR - 4 * (NSTG - 1)); // leading radix 2/4/8/16
-    static constexpr int LS = R + R / 16 + 2;               // LDS line stride (elements)
+    static constexpr int NSTG = (LOGR + 3) / 4;              // radix-16 stages + 1 trailing
+    static constexpr int QL = 1 << (LOGR - 4 * (NSTG - 1));  // trailing radix 2/4/8/16
+    static constexpr int LS = R + R / 16 + 1;                // LDS line stride (odd, scalars)
 };
 
 template <int R, int C>
 struct PassCfg {
     static constexpr int NT = C * R / PassShape<R>::Q;
-    static constexpr int lds_elems = PassShape<R>::NSTG > 1 ? C * PassShape<R>::LS : 0;
+    static constexpr int lds_elems = PassShape<R>::NSTG > 1 ? C * PassShape<R>::LS : 0;  // scalars
+#ifndef PIFFT_MIN_WG_PER_CU
+#define PIFFT_MIN_WG_PER_CU 2
+#endif
+    // register budget: PIFFT_MIN_WG_PER_CU workgroups resident per CU, but
+    // never under 128 VGPRs (4 waves/SIMD): 16 complex values + twiddles
+    static constexpr int wpe = NT >= 256 ? (NT * PIFFT_MIN_WG_PER_CU) / 256 : 1;
+    static constexpr int waves_per_eu = wpe > 4 ? 4 : wpe;
 };
 
-__device__ __forceinline__ int lds_idx(int c, int r, int LS) { return c * LS + r + (r >> 4); }
+__device__ __forceinline__ int lds_pad(int r) { return r + (r >> 4); }
 
-template <typename T, int R, int C>
-__global__ __launch_bounds__((PassCfg<R, C>::NT)) void k_pass(PassArgs a) {
+// v[k] *= w^k (0 < k < q), w^k = w^(k - lowbit k) * w^(lowbit k), anchors
+// a[i] = w^(2^i): chains of <= 3 products, each power applied when formed.
+template <int q, typename T>
+__device__ __forceinline__ void apply_powers(cx<T>* v, const cx<T>* anc) {
+    cx<T> w[q];
+#pragma unroll
+    for (int k = 1; k < q; k++) {
+        const int lb = k & -k;
+        w[k] = (k == lb) ? anc[ilog2c(lb)] : cmul(w[k - lb], w[lb]);
+        v[k] = cmul(v[k], w[k]);
+    }
+}
+
+// Stage S of the R-point sub-FFT in a pass of mode MODE:
+//   radix q (16, the last one 2/4/8/16), U = 16/q butterflies per thread,
+//   NB = R/q butterflies per line, ns = 16^S (product of previous radices).
+// Butterfly g = tid + u*NT maps to (line c, butterfly b) "c-fast" (lanes
+// across lines: the strided side of a pass in HBM) or "b-fast" (lanes along
+// a line: LDS stages and contiguous HBM sides).
+template <int R, int C, int MODE, int S>
+struct Stage {
+    using Sh = PassShape<R>;
+    static constexpr int NT = PassCfg<R, C>::NT;
+    static constexpr bool first = S == 0, last = S == Sh::NSTG - 1;
+    static constexpr int q = last ? Sh::QL : 16;
+    static constexpr int U = Sh::Q / q;
+    static constexpr int NB = R / q;
+    static constexpr int ns = 1 << (4 * S);
+    static constexpr bool cfast = first ? (MODE != 0) : (last ? (MODE == 2) : false);
+    __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
+        const int g = tid + u * NT;
+        if constexpr (cfast) { c = g % C; b = g / C; }
+        else { c = g / NB; b = g % NB; }
+    }
+};
+
+template <typename T, int R, int C, int MODE, int S>
+__device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
-    using S = PassShape<R>;
-    constexpr int Q = S::Q;
-    constexpr int NT = PassCfg<R, C>::NT;
-    constexpr int NSTG = S::NSTG;
-    constexpr int Q0 = S::Q0;
-    constexpr int LS = S::LS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
-    C2* lds = reinterpret_cast<C2*>(pifft_smem);
-
-    const C2* __restrict__ in = static_cast<const C2*>(a.in);
-    C2* __restrict__ out = static_cast<C2*>(a.out);
-    const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
-    const int tid = threadIdx.x;
-    const uint64_t tile = blockIdx.x;
+    using St = Stage<R, C, MODE, S>;
+    using Sh = PassShape<R>;
+    constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns, LS = Sh::LS;
     const uint64_t lb_mask = (1ull << a.log_lb) - 1;
     const uint64_t ns_mask = (1ull << a.log_ns) - 1;
 
-    C2 v[Q];
-
-    // ---- stage 0: radix Q0, straight from HBM ------------------------------
-    {
-        constexpr int q = Q0, U = Q / q, NB = R / q;
-        const bool cfast = a.log_lb > 0;  // lines adjacent in memory -> lanes across lines
+    if constexpr (St::first) {
+        // ---- inputs straight from HBM (all loads issued before any use) ----
+        const C2* __restrict__ in = static_cast<const C2*>(a.in);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int g = tid + u * NT;
-            const int c = cfast ? (g % C) : (g / NB);
-            const int b = cfast ? (g / C) : (g % NB);
+            int c, b;
+            St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             const bool ok = line < a.nlines;
             const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
-            const C2* src = in + bt * a.in_bstride + j;
+            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.log_lb);
 #pragma unroll
-            for (int k = 0; k < q; k++) {
-                const uint64_t r = (uint64_t)(b + k * NB);
-                v[u * q + k] = ok ? src[r << a.log_lb] : C2{(T)0, (T)0};
-            }
-            if (a.log_ns > 0) {  // inter-pass twiddle w_{Ns R}^{(j mod Ns) r}
-                const uint64_t jm = j & ns_mask;
-#pragma unroll
-                for (int k = 0; k < q; k++) {
-                    const uint64_t r = (uint64_t)(b + k * NB);
-                    const uint64_t E = (jm * r) << a.tw_shift;
-                    v[u * q + k] = cmul(v[u * q + k],
-                                        tw2(static_cast<const C2*>(a.tw_lo),
-                                            static_cast<const C2*>(a.tw_hi), a.tw_h, E));
-                }
-            }
-            dft<q>(&v[u * q]);
-            if constexpr (NSTG == 1) {
-                // single stage: outputs r' = k (b == 0) straight to HBM
-                if (ok) {
-                    const uint64_t jm = j & ns_mask;
-                    C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + S::LOGR)) + jm;
-#pragma unroll
-                    for (int k = 0; k < q; k++) {
-                        const uint64_t rp = (uint64_t)(b + k * NB);
-                        dst[rp << a.log_ns] = v[u * q + k];
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < q; k++) lds[lds_idx(c, b * q + k, LS)] = v[u * q + k];
-            }
+            for (int k = 0; k < q; k++)
+                v[u * q + k] = ok ? src[(uint64_t)(k * NB) << a.log_lb] : C2{(T)0, (T)0};
         }
     }
-    if constexpr (NSTG > 1) {
-    __syncthreads();
-
-    // ---- stages 1..NSTG-1: radix 16 through LDS ------------------------------
+    // ---- twiddles before the butterflies ----
+    if constexpr (St::first && MODE == 2) {
+        // w_{Ns R}^{(j mod Ns) r}, r = b + k NB: the k-dependent factor
+        // step^k now, the common factor w^{(j mod Ns) b} after the DFT
+        const C2* tlo = static_cast<const C2*>(a.tw_lo);
+        const C2* thi = static_cast<const C2*>(a.tw_hi);
 #pragma unroll
-    for (int s = 1; s < NSTG; s++) {
-        constexpr int q = 16, NB = R / q;  // one butterfly per thread per line group
-        const int ns = Q0 << (4 * (s - 1));
-        const bool last = (s == NSTG - 1);
-        const bool cfast = last && a.log_ns > 0;
-        const int g = tid;
-        const int c = cfast ? (g % C) : (g / NB);
-        const int b = cfast ? (g / C) : (g % NB);
+        for (int u = 0; u < U; u++) {
+            int c, b;
+            St::map(tid, u, c, b);
+            const uint64_t jm = ((tile * C + c) & lb_mask) & ns_mask;
+            C2 anc[4];
+            anc[0] = tw2(tlo, thi, a.tw_h, (jm * (uint64_t)NB) << a.tw_shift);
 #pragma unroll
-        for (int k = 0; k < q; k++) v[k] = lds[lds_idx(c, b + k * NB, LS)];
-        {   // w_{ns q}^{(b mod ns) k} = w_R^{(b mod ns) k R/(ns q)}
-            const int bm = b & (ns - 1);
-            const int scale = R / (ns * q);
-#pragma unroll
-            for (int k = 1; k < q; k++) v[k] = cmul(v[k], twr[bm * k * scale]);
+            for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
+            apply_powers<q>(&v[u * q], anc);
         }
-        dft<q>(v);
-        if (!last) {
-            __syncthreads();
-            const int base = (b / ns) * ns * q + (b & (ns - 1));
+    }
+    if constexpr (!St::first) {
+        // w_{ns q}^{(b mod ns) k} = w_R^{(b mod ns) k R/(ns q)}
+        const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
 #pragma unroll
-            for (int k = 0; k < q; k++) lds[lds_idx(c, base + k * ns, LS)] = v[k];
-            __syncthreads();
-        } else {
+        for (int u = 0; u < U; u++) {
+            int c, b;
+            St::map(tid, u, c, b);
+            const int e1 = (b & (ns - 1)) * (R / (ns * q));
+            C2 anc[4];
+#pragma unroll
+            for (int i = 0; (1 << i) < q; i++) anc[i] = twr[e1 << i];
+            apply_powers<q>(&v[u * q], anc);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) dft<q>(&v[u * q]);
+    if constexpr (St::first && MODE == 2) {
+        const C2* tlo = static_cast<const C2*>(a.tw_lo);
+        const C2* thi = static_cast<const C2*>(a.tw_hi);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            int c, b;
+            St::map(tid, u, c, b);
+            const uint64_t jm = ((tile * C + c) & lb_mask) & ns_mask;
+            const C2 base = tw2(tlo, thi, a.tw_h, (jm * (uint64_t)b) << a.tw_shift);
+#pragma unroll
+            for (int k = 0; k < q; k++) v[u * q + k] = cmul(v[u * q + k], base);
+        }
+    }
+
+    if constexpr (St::last) {
+        // ---- outputs r' = b + k NB straight to HBM ----
+        C2* __restrict__ out = static_cast<C2*>(a.out);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            int c, b;
+            St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
                 const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
-                const uint64_t jm = j & ns_mask;
-                C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + S::LOGR)) + jm;
+                C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + Sh::LOGR)) + (j & ns_mask) +
+                          ((uint64_t)b << a.log_ns);
 #pragma unroll
-                for (int k = 0; k < q; k++) {
-                    const uint64_t rp = (uint64_t)(b + k * NB);
-                    dst[rp << a.log_ns] = v[k];
+                for (int k = 0; k < q; k++) dst[(uint64_t)(k * NB) << a.log_ns] = v[u * q + k];
+            }
+        }
+    } else {
+        // ---- exchange with stage S+1 through LDS, one component at a time ----
+        using Nx = Stage<R, C, MODE, S + 1>;
+#pragma unroll
+        for (int comp = 0; comp < 2; comp++) {
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                int c, b;
+                St::map(tid, u, c, b);
+                const int base = (b / ns) * ns * q + (b & (ns - 1));  // r' = base + k ns
+#pragma unroll
+                for (int k = 0; k < q; k++) lds[c * LS + lds_pad(base + k * ns)] = comp ? v[u * q + k].im : v[u * q + k].re;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < Nx::U; u++) {
+                int c, b;
+                Nx::map(tid, u, c, b);
+#pragma unroll
+                for (int k = 0; k < Nx::q; k++) {
+                    const T x = lds[c * LS + lds_pad(b + k * Nx::NB)];
+                    if (comp) v[u * Nx::q + k].im = x; else v[u * Nx::q + k].re = x;
                 }
             }
         }
+        pass_stages<T, R, C, MODE, S + 1>(a, lds, v, tid, tile);
     }
-    }  // NSTG > 1
+}
+
+// MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)
+// MODE 1: first pass of several (lines strided in, contiguous out, no twiddle)
+// MODE 2: later pass (strided in and out, inter-pass twiddle)
+template <typename T, int R, int C, int MODE>
+__global__ __launch_bounds__((PassCfg<R, C>::NT), (PassCfg<R, C>::waves_per_eu)) void k_pass(PassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
+    cx<T> v[PassShape<R>::Q];
+    pass_stages<T, R, C, MODE, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------

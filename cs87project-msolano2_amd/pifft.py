@@ -15,7 +15,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpifft.so")
+LIB_PATH = os.environ.get("PIFFT_LIB") or os.path.join(HERE, "libpifft.so")  # PIFFT_LIB: tuning variants
 CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64

@@ -97,6 +97,7 @@ def main() -> None:
     cfg = line["config"]
     key = f"n2^{cfg['n'].bit_length() - 1}_f{b.prec}_b{cfg['batch']}_P{cfg['workers']}_q{cfg['workers_per_gpu']}"
     result["config_key"] = key
+    result["bench_line"] = line
     nl = len(cfg["launches"])
     launch_bytes = [l.get("bytes") for l in cfg["launches"]]
     wide = b.prec == 64
@@ -113,8 +114,9 @@ def main() -> None:
     result["per_launch_bytes"] = out
     result["correction"] = ("FETCH_SIZE KiB x1024 x2 (gfx950 16 B/lane streaming read), WRITE_SIZE KiB x1024"
                             if wide else "uncorrected (8 B/lane accesses uncalibrated)")
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    path = os.path.join(ROOT, "profiles", f"{args.tag}_traffic_{key}.json")
+    # written under gpurun_out/ (merged back from the GPU box); copy into profiles/ to commit
+    os.makedirs(args.outdir, exist_ok=True)
+    path = os.path.join(args.outdir, f"{args.tag}_traffic_{key}.json")
     with open(path, "w") as f:
         json.dump(result, f, indent=1)
     print(json.dumps(result, indent=1))

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""tools/tune.py -- per-launch GB/s of plan variants in one process.
+
+Each variant is a dict of PIFFT_* planner environment variables (read at plan
+creation).  For each: build the plan, run W warm-ups and K timed executions
+with per-launch HIP events, print per-launch ms and algorithmic GB/s.
+
+usage: python tools/tune.py --log-n 28 --prec 64 --variants '[{"PIFFT_COL_C64":"4"}, {}]'
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log-n", type=int, default=28)
+    ap.add_argument("--prec", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--first", type=int, default=0)
+    ap.add_argument("--count", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--variants", default="[{}]")
+    args = ap.parse_args()
+    import torch
+    import pifft
+    n = 1 << args.log_n
+    prec = pifft.F64 if args.prec == 64 else pifft.F32
+    cdt = torch.complex128 if args.prec == 64 else torch.complex64
+    x = torch.empty(n * args.batch, dtype=cdt, device="cuda")
+    pifft.generate_device(x.data_ptr(), n * args.batch, n, prec)
+    y = None
+    # reference ceiling: torch's device copy of the same bytes
+    z = torch.empty_like(x)
+    for _ in range(3):
+        z.copy_(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        z.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    print(f"torch copy: {ms:.3f} ms {2 * x.numel() * x.element_size() / ms / 1e6:.0f} GB/s", flush=True)
+    del z
+    for var in json.loads(args.variants):
+        for k in [k for k in os.environ if k.startswith("PIFFT_")]:
+            del os.environ[k]
+        os.environ.update({k: str(v) for k, v in var.items()})
+        count = args.count or args.workers
+        plan = pifft.Plan(n, args.workers, args.batch, prec, first=args.first, count=count, device=0)
+        d = plan.describe()
+        if y is None or y.numel() != d["out_elems"]:
+            y = torch.empty(d["out_elems"], dtype=cdt, device="cuda")
+        for _ in range(args.warmup):
+            plan.execute_device(x.data_ptr(), y.data_ptr())
+        torch.cuda.synchronize()
+        sums = [0.0] * d["num_launches"]
+        for _ in range(args.steps):
+            for i, m in enumerate(plan.execute_device_timed(x.data_ptr(), y.data_ptr())):
+                sums[i] += m
+        avg = [s / args.steps for s in sums]
+        tot = sum(avg)
+        per = " | ".join(f"{d['launch_kind'][i]} {avg[i]:.3f}ms {d['launch_bytes'][i] / avg[i] / 1e6:.0f}GB/s"
+                         for i in range(d["num_launches"]))
+        gf = 5.0 * n * args.log_n * args.batch / (tot * 1e-3) / 1e9
+        print(f"{json.dumps(var)} radix={d['radix']} lines={d['lines']} total {tot:.3f} ms {gf:.0f} GFLOP/s :: {per}",
+              flush=True)
+        del plan
+
+
+if __name__ == "__main__":
+    main()
