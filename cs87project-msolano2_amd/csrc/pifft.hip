@@ -66,15 +66,15 @@ uint32_t bitrev(uint32_t x, int m) { return m ? (__builtin_bitreverse32(x) >> (3
 // pass kernel instantiations
 // ---------------------------------------------------------------------------
 struct PassKernel {
-    int prec, R, C, mode;
+    int prec, R, C, mode, nts;
     const void* fn;
     int nt;
     int lds_bytes;
 };
 
-#define PK(T, PREC, R, C, MODE)                                                 \
-    PassKernel {                                                                \
-        PREC, R, C, MODE, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE>),\
+#define PK(T, PREC, R, C, MODE, NTS)                                                  \
+    PassKernel {                                                                      \
+        PREC, R, C, MODE, NTS, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS>), \
             PassCfg<R, C>::NT, PassCfg<R, C>::lds_elems * (int)sizeof(T)        \
     }
 
@@ -82,9 +82,9 @@ const PassKernel g_pass_kernels[] = {
 #include "pifft_instances.inc"
 };
 
-const PassKernel* find_pass(int prec, int R, int C, int mode) {
+const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0) {
     for (const auto& k : g_pass_kernels)
-        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode) return &k;
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts) return &k;
     return nullptr;
 }
 
@@ -202,7 +202,7 @@ TwoLevel two_level(TableBuilder& tb, uint64_t L) {
 }
 
 struct PassChoice {
-    int R, C;
+    int R, C, mode, nts;
 };
 
 // Tile = R x C elements per workgroup (C adjacent lines of an R-point sub-FFT).
@@ -214,31 +214,45 @@ int tile_elems(int prec) {
     return env_int(prec == 64 ? "PIFFT_TILE64" : "PIFFT_TILE32", prec == 64 ? 8192 : 16384);
 }
 
-int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, const char* env_c, int mode) {
+int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines, const char* env_c, int mode) {
     int C = env_int(env_c, 0);
     // single pass: lines are whole contiguous transforms, no segment-width
     // constraint -> small tiles (measured best: C = 4096/R, i.e. C=1 at 4096)
-    const int tile = mode == 0 ? env_int(prec == 64 ? "PIFFT_SINGLE_TILE64" : "PIFFT_SINGLE_TILE32", 4096)
-                               : tile_elems(prec);
+    const int tile = mode == 0   ? env_int(prec == 64 ? "PIFFT_SINGLE_TILE64" : "PIFFT_SINGLE_TILE32", 4096)
+                     : mode == 1 ? env_int(prec == 64 ? "PIFFT_FIRST_TILE64" : "PIFFT_FIRST_TILE32", tile_elems(prec))
+                                 : tile_elems(prec);
     if (C <= 0) C = tile / R;
     if (C < 1) C = 1;
     if (C > 64) C = 64;
     if (R <= 8) C = 64;
     while (C > 1 && (uint64_t)C > ntrans_lines_cap && R > 8) C /= 2;
-    while (C > 1 && !find_pass(prec, R, C, mode)) C /= 2;
+    // fill the chip: at least ~2 workgroups per CU (small transforms)
+    const uint64_t min_wg = (uint64_t)env_int("PIFFT_MIN_WORKGROUPS", 512);
+    const int cmin = mode == 0 ? 1 : 4;  // strided passes are instantiated for C >= 4
+    while (C > cmin && R > 8 && total_lines / (uint64_t)C < min_wg) C /= 2;
+    while (C > cmin && !find_pass(prec, R, C, mode)) C /= 2;
     return C;
+}
+
+// non-temporal streaming when a pass moves more than the Infinity Cache holds
+int pick_nts(uint64_t pass_bytes) {
+    const int force = env_int("PIFFT_NT", -1);
+    if (force >= 0) return force ? 1 : 0;
+    return pass_bytes > (256ull << 20) ? 1 : 0;
 }
 
 int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
+    const size_t esz = prec == 64 ? 16 : 8;
+    const int nts = pick_nts(2 * ntrans * M * esz);
     const int single_max = env_int("PIFFT_SINGLE_MAX_LOG", 14);
     if (logm <= single_max) {
         const int R = (int)M;
-        const int C = pick_lines(prec, R, ntrans, prec == 64 ? "PIFFT_SINGLE_C64" : "PIFFT_SINGLE_C32", 0);
-        if (!find_pass(prec, R, C, 0)) return fail("no pass kernel for R=%d C=%d", R, C);
-        out.push_back({R, C});
+        const int C = pick_lines(prec, R, ntrans, ntrans, prec == 64 ? "PIFFT_SINGLE_C64" : "PIFFT_SINGLE_C32", 0);
+        if (!find_pass(prec, R, C, 0, nts)) return fail("no pass kernel for R=%d C=%d", R, C);
+        out.push_back({R, C, 0, nts});
         return 0;
     }
     const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32", 10);
@@ -248,9 +262,10 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         const int bits = base + (p < extra ? 1 : 0);
         const int R = 1 << bits;
         const int mode = p == 0 ? 1 : 2;
-        const int C = pick_lines(prec, R, M >> bits, prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
-        if (!find_pass(prec, R, C, mode)) return fail("no pass kernel for R=%d C=%d mode %d", R, C, mode);
-        out.push_back({R, C});
+        const int C = pick_lines(prec, R, M >> bits, ntrans * (M >> bits),
+                                 prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
+        if (!find_pass(prec, R, C, mode, nts)) return fail("no pass kernel for R=%d C=%d mode %d", R, C, mode);
+        out.push_back({R, C, mode, nts});
     }
     return 0;
 }
@@ -359,8 +374,7 @@ int build_plan(pifft_plan* p) {
     uint64_t ns = 1;
     p->npasses = (int)passes.size();
     for (size_t i = 0; i < passes.size(); i++) {
-        const int mode = passes.size() == 1 ? 0 : (i == 0 ? 1 : 2);
-        const PassKernel* k = find_pass(p->prec, passes[i].R, passes[i].C, mode);
+        const PassKernel* k = find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode, passes[i].nts);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = STEP_PASS;

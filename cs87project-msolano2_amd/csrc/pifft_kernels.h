@@ -146,6 +146,31 @@ __device__ __forceinline__ void dft(cx<T>* v) {
     }
 }
 
+// streamed data: each element is read once and written once per pass.  NTS
+// selects non-temporal (nt) loads/stores for it -- a win when a pass streams
+// more than the 256 MiB Infinity Cache holds, a loss when the data would
+// otherwise stay resident there (measured).
+template <bool NTS, typename T>
+__device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
+    if constexpr (NTS) {
+        cx<T> r;
+        r.re = __builtin_nontemporal_load(&p->re);
+        r.im = __builtin_nontemporal_load(&p->im);
+        return r;
+    } else {
+        return *p;
+    }
+}
+template <bool NTS, typename T>
+__device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
+    if constexpr (NTS) {
+        __builtin_nontemporal_store(v.re, &p->re);
+        __builtin_nontemporal_store(v.im, &p->im);
+    } else {
+        *p = v;
+    }
+}
+
 // two-level twiddle: w_M^E = hi[E >> h] * lo[E & (2^h - 1)]
 template <typename T>
 __device__ __forceinline__ cx<T> tw2(const cx<T>* __restrict__ lo, const cx<T>* __restrict__ hi,
@@ -242,7 +267,7 @@ struct Stage {
     }
 };
 
-template <typename T, int R, int C, int MODE, int S>
+template <typename T, int R, int C, int MODE, bool NTS, int S>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
     using St = Stage<R, C, MODE, S>;
@@ -264,7 +289,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.log_lb);
 #pragma unroll
             for (int k = 0; k < q; k++)
-                v[u * q + k] = ok ? src[(uint64_t)(k * NB) << a.log_lb] : C2{(T)0, (T)0};
+                v[u * q + k] = ok ? ld_stream<NTS>(src + ((uint64_t)(k * NB) << a.log_lb)) : C2{(T)0, (T)0};
         }
     }
     // ---- twiddles before the butterflies ----
@@ -328,7 +353,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + Sh::LOGR)) + (j & ns_mask) +
                           ((uint64_t)b << a.log_ns);
 #pragma unroll
-                for (int k = 0; k < q; k++) dst[(uint64_t)(k * NB) << a.log_ns] = v[u * q + k];
+                for (int k = 0; k < q; k++) st_stream<NTS>(dst + ((uint64_t)(k * NB) << a.log_ns), v[u * q + k]);
             }
         }
     } else {
@@ -357,18 +382,19 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 }
             }
         }
-        pass_stages<T, R, C, MODE, S + 1>(a, lds, v, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, S + 1>(a, lds, v, tid, tile);
     }
 }
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)
 // MODE 1: first pass of several (lines strided in, contiguous out, no twiddle)
 // MODE 2: later pass (strided in and out, inter-pass twiddle)
-template <typename T, int R, int C, int MODE>
+// NTS: non-temporal streaming of the data (see ld_stream)
+template <typename T, int R, int C, int MODE, bool NTS>
 __global__ __launch_bounds__((PassCfg<R, C>::NT), (PassCfg<R, C>::waves_per_eu)) void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     cx<T> v[PassShape<R>::Q];
-    pass_stages<T, R, C, MODE, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x, blockIdx.x);
+    pass_stages<T, R, C, MODE, NTS, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
