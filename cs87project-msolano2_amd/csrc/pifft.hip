@@ -14,6 +14,7 @@
 // the tree uses the reference's own omega(N,k) formula up to N = 2^22 so that
 // its output is bit-identical to the reference's post-tree segment).
 #include "pifft_kernels.h"
+#include "pifft_table.h"
 #include "../../include/pifft.h"
 
 #include <hip/hip_runtime.h>
@@ -63,36 +64,44 @@ int ilog2u(uint64_t x) {
 uint32_t bitrev(uint32_t x, int m) { return m ? (__builtin_bitreverse32(x) >> (32 - m)) : 0u; }
 
 // ---------------------------------------------------------------------------
-// pass kernel instantiations
+// pass kernel instantiations (tables from the pifft_passes.hip parts)
 // ---------------------------------------------------------------------------
-struct PassKernel {
-    int prec, R, C, mode, nts;
-    const void* fn;
-    int nt;
-    int lds_bytes;
-};
+}  // namespace
+#define PIFFT_DECL_PART(k) extern "C" const PassKernel* pifft_pass_table_##k(int* n);
+PIFFT_DECL_PART(0)
+PIFFT_DECL_PART(1)
+PIFFT_DECL_PART(2)
+PIFFT_DECL_PART(3)
+PIFFT_DECL_PART(4)
+PIFFT_DECL_PART(5)
+namespace {
+static_assert(PIFFT_NPART == 6, "update the part list");
 
-#define PK(T, PREC, R, C, MODE, NTS)                                                  \
-    PassKernel {                                                                      \
-        PREC, R, C, MODE, NTS, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS>), \
-            PassCfg<R, C>::NT, PassCfg<R, C>::lds_elems * (int)sizeof(T)        \
-    }
-
-const PassKernel g_pass_kernels[] = {
-#include "pifft_instances.inc"
-};
-
-const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0) {
-    for (const auto& k : g_pass_kernels)
-        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts) return &k;
-    return nullptr;
+const std::vector<PassKernel>& pass_kernels() {
+    static const std::vector<PassKernel> all = [] {
+        std::vector<PassKernel> v;
+        const PassKernel* (*parts[])(int*) = {pifft_pass_table_0, pifft_pass_table_1, pifft_pass_table_2,
+                                               pifft_pass_table_3, pifft_pass_table_4, pifft_pass_table_5};
+        for (auto f : parts) {
+            int n = 0;
+            const PassKernel* t = f(&n);
+            v.insert(v.end(), t, t + n);
+        }
+        return v;
+    }();
+    return all;
 }
 
+const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0) {
+    for (const auto& k : pass_kernels())
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp) return &k;
+    return nullptr;
+}
 
 // ---------------------------------------------------------------------------
 // plan
 // ---------------------------------------------------------------------------
-enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3 };
+enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4 };
 enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, NBUF = 5 };
 
 struct Step {
@@ -120,6 +129,8 @@ struct pifft_plan {
     bool natural = true;
     std::vector<Step> steps;
     int tree_steps = 0, npasses = 0;
+    bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
+    std::vector<Step> tree_only;  // the tree stage alone, for pifft_tree_device
     int radix[8] = {0}, lines[8] = {0};
     void* buf[NBUF] = {nullptr};
     size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0;
@@ -319,6 +330,20 @@ int build_plan(pifft_plan* p) {
     HIPCHK(hipMalloc(&p->d_tw, p->tw_bytes));
     if (!tb.blob.empty()) HIPCHK(hipMemcpy(p->d_tw, tb.blob.data(), tb.blob.size(), hipMemcpyHostToDevice));
     auto twp = [&](size_t off) { return (const void*)((const char*)p->d_tw + off); };
+    TreeTw ttw{};
+    if (need_tree) {
+        ttw.direct = tree_is_direct ? twp(tree_direct) : nullptr;
+        ttw.lo = tree_is_direct ? nullptr : twp(tree2.lo);
+        ttw.hi = tree_is_direct ? nullptr : twp(tree2.hi);
+        ttw.h = tree2.h;
+    }
+    // One worker on this plan, a multi-pass local FFT and log2 P <= 4: fuse the
+    // tree into the first pass (its P leaves per input instead of a separate
+    // tree launch that writes, and a pass that re-reads, the N/P segment).
+    const PassKernel* fused = nullptr;
+    if (need_tree && p->nq == 1 && p->lp <= 4 && passes.size() > 1 && env_int("PIFFT_FUSE_TREE", 1))
+        fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp);
+    p->fused_tree = fused != nullptr;
 
     // --- chain: [tree] [passes] [interleave] ---
     struct Elem { std::vector<Step> steps; };
@@ -347,10 +372,7 @@ int build_plan(pifft_plan* p) {
             s.fn = p->prec == 64 ? tk64[L] : tk32[L];
             s.src = first ? -1 : BUF_TA;  // -1: chain input
             s.dst = last ? -2 : BUF_TA;   // -2: chain output (slice-major)
-            s.ta.tw_direct = tree_is_direct ? twp(tree_direct) : nullptr;
-            s.ta.tw_lo = tree_is_direct ? nullptr : twp(tree2.lo);
-            s.ta.tw_hi = tree_is_direct ? nullptr : twp(tree2.hi);
-            s.ta.tw_h = tree2.h;
+            s.ta.tw = ttw;
             s.ta.in_bstride = p->n;
             s.ta.out_bstride = last ? (uint64_t)p->nq * M : p->n;
             s.ta.out_shift = last ? -(int64_t)((uint64_t)p->q0 * M) : 0;
@@ -368,23 +390,37 @@ int build_plan(pifft_plan* p) {
             t0 += L;
         }
         if (nl > 1) p->bytes_ta = (size_t)p->batch * p->n * esz;
-        p->tree_steps = (int)e.steps.size();
-        chain.push_back(e);
+        // the stand-alone tree (pifft_tree_device) reads d_in and writes d_seg
+        for (Step t : e.steps) {
+            if (t.src == -1) t.src = BUF_IN;
+            if (t.dst == -2) t.dst = BUF_OUT;
+            p->tree_only.push_back(t);
+        }
+        if (!fused) {
+            p->tree_steps = (int)e.steps.size();
+            chain.push_back(e);
+        }
     }
     uint64_t ns = 1;
     p->npasses = (int)passes.size();
     for (size_t i = 0; i < passes.size(); i++) {
-        const PassKernel* k = find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode, passes[i].nts);
+        const bool fuse_here = (i == 0 && fused);
+        const PassKernel* k = fuse_here ? fused
+                                        : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode, passes[i].nts);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
-        s.kind = STEP_PASS;
+        s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
         s.fn = k->fn;
         const int logr = ilog2u((uint64_t)k->R);
         s.pa.tw_r = twp(tw_r[i]);
         s.pa.tw_lo = passes.size() > 1 ? twp(pass2.lo) : nullptr;
         s.pa.tw_hi = passes.size() > 1 ? twp(pass2.hi) : nullptr;
         s.pa.tw_h = pass2.h;
-        s.pa.in_bstride = (i == 0 && !need_tree) ? p->n : M;
+        s.pa.in_bstride = (i == 0 && (!need_tree || fuse_here)) ? p->n : M;
+        if (fuse_here) {
+            s.pa.tree = ttw;
+            s.pa.worker = p->q0;
+        }
         s.pa.out_bstride = M;
         s.pa.nlines = ntrans * (M >> logr);
         s.pa.log_lb = (uint32_t)(p->log_m - logr);
@@ -393,7 +429,7 @@ int build_plan(pifft_plan* p) {
         s.block = dim3((unsigned)k->nt);
         s.grid = dim3((unsigned)((s.pa.nlines + k->C - 1) / k->C));
         s.lds = (size_t)k->lds_bytes;
-        s.bytes = 2 * ntrans * M * esz;
+        s.bytes = fuse_here ? (uint64_t)p->batch * (p->n + M) * esz : 2 * ntrans * M * esz;
         if (s.lds > 65536) (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {
             p->radix[i] = k->R;
@@ -497,7 +533,8 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
     char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
     hipError_t e = hipSuccess;
     switch (s.kind) {
-        case STEP_PASS: {
+        case STEP_PASS:
+        case STEP_TREE_PASS: {
             PassArgs a = s.pa;
             a.in = src;
             a.out = dst;
@@ -554,7 +591,8 @@ int run_timed(pifft_plan* p, const void* d_in, void* d_out, hipStream_t st, std:
 
 void stage_split(const pifft_plan* p, const std::vector<float>& ms, double* s1, double* s2) {
     double a = 0, b = 0;
-    for (size_t i = 0; i < ms.size(); i++) (p->steps[i].kind == STEP_TREE ? a : b) += ms[i];
+    for (size_t i = 0; i < ms.size(); i++)
+        (p->steps[i].kind == STEP_TREE || p->steps[i].kind == STEP_TREE_PASS ? a : b) += ms[i];
     if (s1) *s1 = a;
     if (s2) *s2 = b;
 }
@@ -770,16 +808,12 @@ int pifft_tree_device(pifft_plan* p, const void* d_in, void* d_seg, void* stream
     if (check_buffers(p, d_in, d_seg)) return -1;
     DeviceGuard g(p->device);
     hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
-    if (p->tree_steps == 0) {  // P == 1: the segment is the input
+    if (p->tree_only.empty()) {  // P == 1: the segment is the input
         HIPCHK(hipMemcpyAsync(d_seg, d_in, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToDevice, st));
         return 0;
     }
-    for (int i = 0; i < p->tree_steps; i++) {
-        Step s = p->steps[i];
-        if (s.dst != BUF_TA) s.dst = BUF_OUT;
-        if (s.src != BUF_TA) s.src = BUF_IN;
+    for (const Step& s : p->tree_only)
         if (launch_step(p, s, d_in, d_seg, st)) return -1;
-    }
     return 0;
 }
 

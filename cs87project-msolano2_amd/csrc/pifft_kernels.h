@@ -181,6 +181,80 @@ __device__ __forceinline__ cx<T> tw2(const cx<T>* __restrict__ lo, const cx<T>* 
 }
 
 // ---------------------------------------------------------------------------
+// Tree ("funnel") network, shared by k_tree and the fused first pass
+// ---------------------------------------------------------------------------
+struct TreeTw {
+    const void* direct;  // omega(N, e), e < N/2, the reference formula (CPU.c:644-651); or null
+    const void* lo;      // else two-level w_N
+    const void* hi;
+    uint32_t h;
+};
+
+template <typename T>
+__device__ __forceinline__ cx<T> tree_tw(const TreeTw& tw, uint64_t e) {
+    if (tw.direct) return static_cast<const cx<T>*>(tw.direct)[e];
+    return tw2(static_cast<const cx<T>*>(tw.lo), static_cast<const cx<T>*>(tw.hi), tw.h, e);
+}
+
+// Levels t0 .. t0+L-1 of the reference's radix-2 tree (CPU.c:419-448; level t
+// is the butterfly of size N >> t) on the 2^L values a thread holds at
+// positions base + i + m*2^log_d.  After the last of these levels v[m] lies
+// in the block leading to workers [((blk0 << L) + m) << log_w, +2^log_w);
+// only branches leading to workers [q0, q1) are evaluated (uniform branches,
+// compile-time register indices).  Operation order = butterfly_left /
+// butterfly_right (CPU.c:540-576): add, or (sub) * omega.
+template <typename T, int L>
+__device__ __forceinline__ void tree_levels(cx<T>* v, const TreeTw& tw, uint64_t i, uint32_t log_d, uint32_t t0,
+                                            uint64_t blk0, uint32_t log_w, uint64_t q0, uint64_t q1) {
+    constexpr int V = 1 << L;
+#pragma unroll
+    for (int tl = 0; tl < L; tl++) {
+        const int BS = V >> tl, H = BS >> 1;
+        const uint32_t t = t0 + tl;
+#pragma unroll
+        for (int blk = 0; blk < (1 << tl); blk++) {
+            const int lo = blk * BS;
+            const uint64_t cl0 = (((blk0 << L) + lo) << log_w), cl1 = (((blk0 << L) + lo + H) << log_w);
+            const uint64_t cr1 = (((blk0 << L) + lo + BS) << log_w);
+            const bool needL = (cl0 < q1) && (cl1 > q0);
+            const bool needR = (cl1 < q1) && (cr1 > q0);
+#pragma unroll
+            for (int ml = 0; ml < H; ml++) {
+                const cx<T> x0 = v[lo + ml], x1 = v[lo + ml + H];
+                if (needL) v[lo + ml] = cadd(x0, x1);                      // butterfly_left
+                if (needR) {                                               // butterfly_right
+                    const uint64_t e = (i + ((uint64_t)ml << log_d)) << t;  // b * N/size
+                    v[lo + ml + H] = cmul(csub(x0, x1), tree_tw<T>(tw, e));
+                }
+            }
+        }
+    }
+}
+
+// The tree for ONE worker q (the reference's run_thread view, CPU.c:419-448):
+// v[m] = x[i + m M] (m < P); level t keeps the left half (add) or the right
+// half ((sub) * omega(N, b 2^t)) as bit log2P-1-t of q says (CPU.c:429), the
+// kept half compacted into v[0 .. P>>(t+1)).  One uniform branch per level.
+template <typename T, int LP>
+__device__ __forceinline__ cx<T> tree_path(cx<T>* v, const TreeTw& tw, uint64_t i, uint32_t log_m, uint32_t q) {
+#pragma unroll
+    for (int t = 0; t < LP; t++) {
+        const int H = (1 << LP) >> (t + 1);
+        if ((q >> (LP - 1 - t)) & 1) {
+#pragma unroll
+            for (int ml = 0; ml < H; ml++) {
+                const uint64_t e = (i + ((uint64_t)ml << log_m)) << t;
+                v[ml] = cmul(csub(v[ml], v[ml + H]), tree_tw<T>(tw, e));
+            }
+        } else {
+#pragma unroll
+            for (int ml = 0; ml < H; ml++) v[ml] = cadd(v[ml], v[ml + H]);
+        }
+    }
+    return v[0];
+}
+
+// ---------------------------------------------------------------------------
 // Stockham pass
 // ---------------------------------------------------------------------------
 // One pass of the local FFT (Stockham auto-sort, natural order in and out):
@@ -205,6 +279,10 @@ struct PassArgs {
     uint32_t log_ns;      // log2 Ns (product of the radices of the previous passes)
     uint32_t tw_h;        // bits of the low twiddle table
     uint32_t tw_shift;    // log2(M / (Ns R))
+    // MODE 3 (tree fused into the first pass): worker q of P = 2^LP, leaves
+    // x[i + m M], in_bstride = N
+    TreeTw tree;
+    uint32_t worker;
 };
 
 template <int R>
@@ -259,7 +337,7 @@ struct Stage {
     static constexpr int U = Sh::Q / q;
     static constexpr int NB = R / q;
     static constexpr int ns = 1 << (4 * S);
-    static constexpr bool cfast = first ? (MODE != 0) : (last ? (MODE == 2) : false);
+    static constexpr bool cfast = first ? (MODE != 0) : (last ? (MODE == 2) : false);  // MODE 3 as MODE 1
     __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
         const int g = tid + u * NT;
         if constexpr (cfast) { c = g % C; b = g / C; }
@@ -267,7 +345,7 @@ struct Stage {
     }
 };
 
-template <typename T, int R, int C, int MODE, bool NTS, int S>
+template <typename T, int R, int C, int MODE, bool NTS, int LP, int S>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
     using St = Stage<R, C, MODE, S>;
@@ -287,9 +365,35 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const bool ok = line < a.nlines;
             const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
             const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.log_lb);
+            if constexpr (MODE == 3) {
+                // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
+                // G elements (G*P = 8 loads in flight) per round: no spills up
+                // to P = 8 at 128 VGPRs
+                constexpr int P = 1 << LP;
+                constexpr int G = P >= 8 ? 1 : 8 / P;
+                const uint32_t log_m = a.log_lb + Sh::LOGR;
 #pragma unroll
-            for (int k = 0; k < q; k++)
-                v[u * q + k] = ok ? ld_stream<NTS>(src + ((uint64_t)(k * NB) << a.log_lb)) : C2{(T)0, (T)0};
+                for (int k0 = 0; k0 < q; k0 += G) {
+                    C2 w[G][P];
+#pragma unroll
+                    for (int g = 0; g < G; g++) {
+                        const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << a.log_lb);
+#pragma unroll
+                        for (int m = 0; m < P; m++)
+                            w[g][m] = ok ? ld_stream<NTS>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
+                    }
+#pragma unroll
+                    for (int g = 0; g < G; g++) {
+                        const uint64_t zi = j + ((uint64_t)(b + (k0 + g) * NB) << a.log_lb);
+                        v[u * q + k0 + g] = tree_path<T, LP>(w[g], a.tree, zi, log_m, a.worker);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < q; k++)
+                    v[u * q + k] = ok ? ld_stream<NTS>(src + ((uint64_t)(k * NB) << a.log_lb)) : C2{(T)0, (T)0};
+            }
         }
     }
     // ---- twiddles before the butterflies ----
@@ -382,19 +486,23 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 }
             }
         }
-        pass_stages<T, R, C, MODE, NTS, S + 1>(a, lds, v, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1>(a, lds, v, tid, tile);
     }
 }
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)
 // MODE 1: first pass of several (lines strided in, contiguous out, no twiddle)
 // MODE 2: later pass (strided in and out, inter-pass twiddle)
+// MODE 3: first pass with the tree stage fused in (one worker, P = 2^LP):
+//         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // NTS: non-temporal streaming of the data (see ld_stream)
-template <typename T, int R, int C, int MODE, bool NTS>
-__global__ __launch_bounds__((PassCfg<R, C>::NT), (PassCfg<R, C>::waves_per_eu)) void k_pass(PassArgs a) {
+template <typename T, int R, int C, int MODE, bool NTS, int LP>
+__global__ __launch_bounds__((PassCfg<R, C>::NT),
+                             (MODE == 3 && LP >= 4 && PassCfg<R, C>::waves_per_eu > 2 ? 2 : PassCfg<R, C>::waves_per_eu))
+void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     cx<T> v[PassShape<R>::Q];
-    pass_stages<T, R, C, MODE, NTS, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x, blockIdx.x);
+    pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -411,23 +519,14 @@ __global__ __launch_bounds__((PassCfg<R, C>::NT), (PassCfg<R, C>::waves_per_eu))
 struct TreeArgs {
     const void* in;
     void* out;
-    const void* tw_direct;  // omega(N, e), e < N/2, reference formula; or null
-    const void* tw_lo;      // else two-level w_N
-    const void* tw_hi;
+    TreeTw tw;
     uint64_t in_bstride;    // N
     uint64_t out_bstride;   // N (position space) or nq * N/P (slice-major)
     int64_t out_shift;      // 0 or -q0 * N/P
     uint64_t total;         // transforms * (N >> L)
     uint32_t log_n, log_p, t0;
-    uint32_t tw_h;
     uint32_t q0, nq;        // workers [q0, q0+nq)
 };
-
-template <typename T>
-__device__ __forceinline__ cx<T> tree_tw(const TreeArgs& a, uint64_t e) {
-    if (a.tw_direct) return static_cast<const cx<T>*>(a.tw_direct)[e];
-    return tw2(static_cast<const cx<T>*>(a.tw_lo), static_cast<const cx<T>*>(a.tw_hi), a.tw_h, e);
-}
 
 template <typename T, int L>
 __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
@@ -440,9 +539,7 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
     const uint64_t g = gid & ((1ull << log_g) - 1), bt = gid >> log_g;
     const uint64_t blk0 = g >> log_d, i = g & ((1ull << log_d) - 1);
     const uint64_t base = blk0 << (a.log_n - a.t0);
-    // v[m] ends in the level-(t0+L) block (blk0 << L) + m, which leads to
-    // workers [((blk0 << L) + m) W, +W), W = P >> (t0 + L)
-    const uint32_t log_w = a.log_p - a.t0 - L;
+    const uint32_t log_w = a.log_p - a.t0 - L;     // workers below one level-(t0+L) block
     const uint64_t q0 = a.q0, q1 = (uint64_t)a.q0 + a.nq;
     const uint64_t w_lo = (blk0 << L) << log_w, w_hi = ((blk0 + 1) << L) << log_w;
     if (w_hi <= q0 || w_lo >= q1) return;  // no requested worker below this group
@@ -450,28 +547,7 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
     C2 v[V];
 #pragma unroll
     for (int m = 0; m < V; m++) v[m] = src[(uint64_t)m << log_d];
-#pragma unroll
-    for (int tl = 0; tl < L; tl++) {
-        const int BS = V >> tl, H = BS >> 1;
-        const uint32_t t = a.t0 + tl;  // global level: butterfly size N >> t
-#pragma unroll
-        for (int blk = 0; blk < (1 << tl); blk++) {
-            const int lo = blk * BS;
-            const uint64_t cl0 = (((blk0 << L) + lo) << log_w), cl1 = (((blk0 << L) + lo + H) << log_w);
-            const uint64_t cr1 = (((blk0 << L) + lo + BS) << log_w);
-            const bool needL = (cl0 < q1) && (cl1 > q0);
-            const bool needR = (cl1 < q1) && (cr1 > q0);
-#pragma unroll
-            for (int ml = 0; ml < H; ml++) {
-                const C2 x0 = v[lo + ml], x1 = v[lo + ml + H];
-                if (needL) v[lo + ml] = cadd(x0, x1);                         // butterfly_left
-                if (needR) {                                                  // butterfly_right
-                    const uint64_t e = (i + ((uint64_t)ml << log_d)) << t;    // b * N/size
-                    v[lo + ml + H] = cmul(csub(x0, x1), tree_tw<T>(a, e));
-                }
-            }
-        }
-    }
+    tree_levels<T, L>(v, a.tw, i, log_d, a.t0, blk0, log_w, q0, q1);
     C2* __restrict__ dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (int64_t)(base + i) + a.out_shift;
 #pragma unroll
     for (int m = 0; m < V; m++) {

@@ -20,7 +20,7 @@ CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64
 OUT_NATURAL, OUT_SLICES = 0, 1
-KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave"}
+KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass"}
 
 
 class PifftError(RuntimeError):
@@ -83,7 +83,7 @@ _lib = None
 
 def build(quiet: bool = True) -> None:
     """hipcc --offload-arch=gfx950 -> libpifft.so, gcc -> the pifft CLI (in-tree)."""
-    subprocess.run(["make", "-C", HERE, "all"], check=True,
+    subprocess.run(["make", "-j8", "-C", HERE, "all"], check=True,
                    stdout=subprocess.DEVNULL if quiet else None)
 
 

@@ -68,7 +68,7 @@ typedef struct pifft_plan_info {
     int32_t lines[8];        /* columns per workgroup of each pass                 */
     uint64_t launch_bytes[64]; /* algorithmic HBM bytes of each launch (read+write,
                                   twiddle tables excluded)                         */
-    int32_t launch_kind[64]; /* 1 tree, 2 pass, 3 interleave                      */
+    int32_t launch_kind[64]; /* 1 tree, 2 pass, 3 interleave, 4 tree fused into a pass */
 } pifft_plan_info;
 
 /* Last error message of the calling thread ("" if none). */

@@ -346,3 +346,25 @@ def test_cli_tsv_and_dump(tmp_path):
     got = np.fromfile(out, dtype=np.complex128)
     x = oracle.generate(4096, np.complex128, seed=7)
     assert_bins_close(got, oracle.fft(x, P=4), "f64", 4096)
+
+
+# ------------------------------------------------- fused tree + first pass ---
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("logn,P", [(16, 2), (18, 4), (19, 8), (20, 16), (23, 8)])
+def test_fused_tree_first_pass(suf, logn, P, monkeypatch):
+    """Single-worker plans with a multi-pass local FFT evaluate the tree inside
+    the first pass (MODE 3); results must match the oracle and the unfused plan."""
+    n = 1 << logn
+    x = oracle.generate(n, DT[suf], seed=logn * 7 + P)
+    want = oracle.fft(x, P=1, nthreads=8)
+    for q in sorted({0, (P // 2 + 1) % P, P - 1}):
+        fused = pifft.Plan(n, P, 1, PREC[suf], first=q, count=1, device=0)
+        kinds = fused.describe()["launch_kind"]
+        assert "tree" not in kinds, kinds  # fused: no separate tree launch
+        got = run(fused, x)
+        assert_bins_close(got, pifft_dist.slice_of_natural(want, P, q), suf, n)
+        monkeypatch.setenv("PIFFT_FUSE_TREE", "0")
+        plain = pifft.Plan(n, P, 1, PREC[suf], first=q, count=1, device=0)
+        monkeypatch.delenv("PIFFT_FUSE_TREE")
+        assert plain.describe()["launch_kind"][0] == "tree"
+        assert rel_l2(run(plain, x), got) <= tol(suf, n)
