@@ -103,6 +103,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-log-n", type=int, default=26)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0 (use with --dist-backend gloo)")
     args = ap.parse_args()
 
     import torch
@@ -111,16 +114,23 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = 0 if args.same_device else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     def barrier():
         if dist is not None:
-            dist.barrier(device_ids=[local])
+            if args.dist_backend == "nccl":
+                dist.barrier(device_ids=[gpu])
+            else:
+                dist.barrier()
 
     n = 1 << args.log_n
     P = args.workers or world
@@ -131,9 +141,9 @@ def main() -> None:
     esz = 16 if prec == pifft.F64 else 8
 
     if count == P:
-        plan = pifft.Plan(n, P, args.batch, prec, first=0, count=P, device=local, flags=pifft.OUT_NATURAL)
+        plan = pifft.Plan(n, P, args.batch, prec, first=0, count=P, device=gpu, flags=pifft.OUT_NATURAL)
     else:
-        plan = pifft.Plan(n, P, args.batch, prec, first=first, count=count, device=local,
+        plan = pifft.Plan(n, P, args.batch, prec, first=first, count=count, device=gpu,
                           flags=pifft.OUT_SLICES)
     desc = plan.describe()
     stream = torch.cuda.current_stream(dev)
@@ -156,7 +166,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    elapsed = pifft_dist.max_over_ranks(elapsed, dev)
+    red_dev = dev if args.dist_backend == "nccl" else None  # gloo reduces on the CPU
+    elapsed = pifft_dist.max_over_ranks(elapsed, red_dev)
     ms_per_step = elapsed * 1e3 / args.steps
 
     allgather_ms = None
@@ -168,7 +179,7 @@ def main() -> None:
         natural = torch.empty(n * args.batch, dtype=cdt, device=dev)
         pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), n, P, args.batch, prec, stream)
         torch.cuda.synchronize(dev)
-        allgather_ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, dev)
+        allgather_ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
         del gathered, natural
 
     avg = [s / args.steps for s in sums]

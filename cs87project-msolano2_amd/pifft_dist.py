@@ -51,9 +51,14 @@ def allgather_slices(local, group=None):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    parts = [torch.empty_like(local) for _ in range(world)]
-    dist.all_gather(parts, local.contiguous(), group=group)
-    return torch.cat(parts)
+    src = local.contiguous()
+    staged = dist.get_backend(group) == "gloo" and src.is_cuda  # gloo gathers host tensors
+    if staged:
+        src = src.cpu()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    out = torch.cat(parts)
+    return out.to(local.device) if staged else out
 
 
 def max_over_ranks(value: float, device=None) -> float:
