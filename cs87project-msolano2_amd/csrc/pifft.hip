@@ -56,6 +56,13 @@ int env_int(const char* name, int dflt) {
 }
 
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+// 1-D grid for a grid-stride kernel of `total` items at 256 threads/block:
+// capped so the launch's work-item count stays far below 2^32
+unsigned stride_grid(uint64_t total) {
+    const uint64_t blocks = (total + 255) / 256;
+    return (unsigned)(blocks < 262144 ? (blocks ? blocks : 1) : 262144);
+}
 int ilog2u(uint64_t x) {
     int l = 0;
     while (x > 1) { x >>= 1; l++; }
@@ -252,7 +259,9 @@ int pick_nts(uint64_t pass_bytes) {
     return pass_bytes > (256ull << 20) ? 1 : 0;
 }
 
-int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out) {
+// heavy_first: the first pass carries extra reads (the fused tree reads P
+// leaves per input), so it gets the smallest radix -> the widest line group.
+int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, bool heavy_first = false) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
@@ -270,7 +279,9 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
     const int k = (logm + rmax_log - 1) / rmax_log;
     const int base = logm / k, extra = logm % k;
     for (int p = 0; p < k; p++) {
-        const int bits = base + (p < extra ? 1 : 0);
+        // larger radices first (the first pass has one contiguous side), or
+        // smallest first when the first pass is the heavy one
+        const int bits = heavy_first ? base + (p >= k - extra ? 1 : 0) : base + (p < extra ? 1 : 0);
         const int R = 1 << bits;
         const int mode = p == 0 ? 1 : 2;
         const int C = pick_lines(prec, R, M >> bits, ntrans * (M >> bits),
@@ -298,7 +309,8 @@ int build_plan(pifft_plan* p) {
     const size_t esz = p->esz;
     const uint64_t ntrans = (uint64_t)p->batch * p->nq;  // local transforms
     std::vector<PassChoice> passes;
-    if (plan_passes(p->m, p->prec, ntrans, passes)) return -1;
+    const bool may_fuse = p->P > 1 && p->nq == 1 && p->lp <= 4 && env_int("PIFFT_FUSE_TREE", 1);
+    if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse)) return -1;
 
     TableBuilder tb(esz);
     // --- tree tables (w_N) ---
@@ -341,7 +353,7 @@ int build_plan(pifft_plan* p) {
     // tree into the first pass (its P leaves per input instead of a separate
     // tree launch that writes, and a pass that re-reads, the N/P segment).
     const PassKernel* fused = nullptr;
-    if (need_tree && p->nq == 1 && p->lp <= 4 && passes.size() > 1 && env_int("PIFFT_FUSE_TREE", 1))
+    if (may_fuse && passes.size() > 1)
         fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp);
     p->fused_tree = fused != nullptr;
 
@@ -383,7 +395,7 @@ int build_plan(pifft_plan* p) {
             s.ta.q0 = p->q0;
             s.ta.nq = p->nq;
             s.block = dim3(256);
-            s.grid = dim3((unsigned)((s.ta.total + 255) / 256));
+            s.grid = dim3(stride_grid(s.ta.total));
             s.bytes = (uint64_t)p->batch * esz *
                       (blocks_needed(t0) * (p->n >> t0) + blocks_needed(t0 + L) * (p->n >> (t0 + L)));
             e.steps.push_back(s);
@@ -427,7 +439,10 @@ int build_plan(pifft_plan* p) {
         s.pa.log_ns = (uint32_t)ilog2u(ns);
         s.pa.tw_shift = (uint32_t)(p->log_m - ilog2u(ns) - logr);
         s.block = dim3((unsigned)k->nt);
-        s.grid = dim3((unsigned)((s.pa.nlines + k->C - 1) / k->C));
+        const uint64_t wgs = (s.pa.nlines + k->C - 1) / k->C;
+        if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
+                                                             (unsigned long long)(wgs * k->nt));
+        s.grid = dim3((unsigned)wgs);
         s.lds = (size_t)k->lds_bytes;
         s.bytes = fuse_here ? (uint64_t)p->batch * (p->n + M) * esz : 2 * ntrans * M * esz;
         if (s.lds > 65536) (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
@@ -448,7 +463,7 @@ int build_plan(pifft_plan* p) {
         s.il_log_n = (uint32_t)p->log_n;
         s.il_log_p = (uint32_t)p->lp;
         s.block = dim3(256);
-        s.grid = dim3((unsigned)((s.il_total + 255) / 256));
+        s.grid = dim3(stride_grid(s.il_total));
         s.bytes = 2 * s.il_total * esz;
         Elem e;
         e.steps.push_back(s);
@@ -774,7 +789,7 @@ int pifft_generate_device(void* d_x, uint64_t count, uint64_t n, uint64_t seed, 
     if (prec != PIFFT_F32 && prec != PIFFT_F64) return fail("bad precision");
     if (count == 0) return 0;
     const double scale = sqrt((double)n);
-    const dim3 blk(256), grd((unsigned)((count + 255) / 256));
+    const dim3 blk(256), grd(stride_grid(count));
     hipStream_t st = (hipStream_t)stream;
     if (prec == PIFFT_F64)
         hipLaunchKernelGGL(k_generate<double>, grd, blk, 0, st, (cx<double>*)d_x, count, scale, seed, first);
@@ -789,7 +804,7 @@ int pifft_interleave_device(const void* d_slices, void* d_out, uint64_t n, uint3
     if (!d_slices || !d_out || d_slices == d_out) return fail("bad buffers");
     if (n < 2 || !is_pow2(n) || !workers || !is_pow2(workers) || workers > n) return fail("bad n/workers");
     const uint64_t total = (uint64_t)batch * n;
-    const dim3 blk(256), grd((unsigned)((total + 255) / 256));
+    const dim3 blk(256), grd(stride_grid(total));
     hipStream_t st = (hipStream_t)stream;
     const uint32_t ln = (uint32_t)ilog2u(n), lpp = (uint32_t)ilog2u(workers);
     if (prec == PIFFT_F64)

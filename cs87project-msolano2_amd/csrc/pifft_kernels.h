@@ -532,8 +532,9 @@ template <typename T, int L>
 __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
     using C2 = cx<T>;
     constexpr int V = 1 << L;
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= a.total) return;
+    // grid-stride: the work-item count of one launch must stay below 2^32
+    for (uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < a.total;
+         gid += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t log_g = a.log_n - L;            // threads per transform = 2^log_g
     const uint32_t log_d = a.log_n - a.t0 - L;     // D = stride between a thread's positions
     const uint64_t g = gid & ((1ull << log_g) - 1), bt = gid >> log_g;
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
     const uint32_t log_w = a.log_p - a.t0 - L;     // workers below one level-(t0+L) block
     const uint64_t q0 = a.q0, q1 = (uint64_t)a.q0 + a.nq;
     const uint64_t w_lo = (blk0 << L) << log_w, w_hi = ((blk0 + 1) << L) << log_w;
-    if (w_hi <= q0 || w_lo >= q1) return;  // no requested worker below this group
+    if (w_hi <= q0 || w_lo >= q1) continue;  // no requested worker below this group
     const C2* __restrict__ src = static_cast<const C2*>(a.in) + bt * a.in_bstride + base + i;
     C2 v[V];
 #pragma unroll
@@ -554,6 +555,7 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
         const uint64_t wm = ((blk0 << L) + m) << log_w;
         if (wm < q1 && wm + (1ull << log_w) > q0) dst[(uint64_t)m << log_d] = v[m];
     }
+    }  // grid-stride
 }
 
 // ---------------------------------------------------------------------------
@@ -563,14 +565,15 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_interleave(const cx<T>* __restrict__ in,
                                                     cx<T>* __restrict__ out, uint64_t total,
                                                     uint32_t log_n, uint32_t log_p) {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= total) return;
     const uint64_t n = 1ull << log_n;
-    const uint64_t bt = gid >> log_n, o = gid & (n - 1);
-    const uint64_t k = o >> log_p;
-    const uint32_t rr = (uint32_t)(o & ((1ull << log_p) - 1));
-    const uint32_t q = log_p ? (__builtin_bitreverse32(rr) >> (32 - log_p)) : 0u;
-    out[gid] = in[bt * n + ((uint64_t)q << (log_n - log_p)) + k];
+    for (uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+         gid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t bt = gid >> log_n, o = gid & (n - 1);
+        const uint64_t k = o >> log_p;
+        const uint32_t rr = (uint32_t)(o & ((1ull << log_p) - 1));
+        const uint32_t q = log_p ? (__builtin_bitreverse32(rr) >> (32 - log_p)) : 0u;
+        out[gid] = in[bt * n + ((uint64_t)q << (log_n - log_p)) + k];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -586,12 +589,13 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t draw) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_generate(cx<T>* __restrict__ x, uint64_t count,
                                                   double scale, uint64_t seed, uint64_t first) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= count) return;
-    const uint64_t d = 2 * (first + e);
-    const double ur = (double)(splitmix64(seed, d) >> 11) * 0x1.0p-53;
-    const double ui = (double)(splitmix64(seed, d + 1) >> 11) * 0x1.0p-53;
-    x[e] = cx<T>{(T)((2.0 * ur - 1.0) / scale), (T)((2.0 * ui - 1.0) / scale)};
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = 2 * (first + e);
+        const double ur = (double)(splitmix64(seed, d) >> 11) * 0x1.0p-53;
+        const double ui = (double)(splitmix64(seed, d + 1) >> 11) * 0x1.0p-53;
+        x[e] = cx<T>{(T)((2.0 * ur - 1.0) / scale), (T)((2.0 * ui - 1.0) / scale)};
+    }
 }
 
 }  // namespace pifft
