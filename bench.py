@@ -155,17 +155,19 @@ def main() -> None:
     torch.cuda.synchronize(dev)
 
     nl = desc["num_launches"]
-    sums = [0.0] * nl
+    # per-launch HIP events on the launch stream, recorded inside the timed
+    # region without host syncs (pifft_profile_start/read)
+    plan.profile_start(args.steps)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ms = plan.execute_device_timed(x.data_ptr(), y.data_ptr(), stream)
-        for i, m in enumerate(ms):
-            sums[i] += m
+        plan.execute_device(x.data_ptr(), y.data_ptr(), stream)
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
+    recorded, sums = plan.profile_read()
+    assert recorded == args.steps, recorded
     red_dev = dev if args.dist_backend == "nccl" else None  # gloo reduces on the CPU
     elapsed = pifft_dist.max_over_ranks(elapsed, red_dev)
     ms_per_step = elapsed * 1e3 / args.steps

@@ -138,6 +138,8 @@ struct pifft_plan {
     int tree_steps = 0, npasses = 0;
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
     std::vector<Step> tree_only;  // the tree stage alone, for pifft_tree_device
+    std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: steps x (launches + 1)
+    int prof_steps = 0, prof_used = 0;
     int radix[8] = {0}, lines[8] = {0};
     void* buf[NBUF] = {nullptr};
     size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0;
@@ -301,6 +303,7 @@ void release(pifft_plan* p) {
     if (p->d_hin) (void)hipFree(p->d_hin);
     if (p->d_hout) (void)hipFree(p->d_hout);
     for (auto e : p->ev) (void)hipEventDestroy(e);
+    for (auto e : p->prof_ev) (void)hipEventDestroy(e);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -438,6 +441,7 @@ int build_plan(pifft_plan* p) {
         s.pa.log_lb = (uint32_t)(p->log_m - logr);
         s.pa.log_ns = (uint32_t)ilog2u(ns);
         s.pa.tw_shift = (uint32_t)(p->log_m - ilog2u(ns) - logr);
+        s.pa.log_xg = (uint32_t)env_int(passes[i].mode == 0 ? "PIFFT_XCD_GROUP_SINGLE" : "PIFFT_XCD_GROUP", passes[i].mode == 0 ? 0 : 2);
         s.block = dim3((unsigned)k->nt);
         const uint64_t wgs = (s.pa.nlines + k->C - 1) / k->C;
         if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
@@ -701,9 +705,50 @@ int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* str
     if (check_buffers(p, d_in, d_out)) return -1;
     DeviceGuard g(p->device);
     hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
-    for (const auto& s : p->steps)
-        if (launch_step(p, s, d_in, d_out, st)) return -1;
+    const size_t ns = p->steps.size();
+    hipEvent_t* ev = nullptr;
+    if (p->prof_used < p->prof_steps) ev = &p->prof_ev[(size_t)p->prof_used++ * (ns + 1)];
+    for (size_t i = 0; i < ns; i++) {
+        if (ev) HIPCHK(hipEventRecord(ev[i], st));
+        if (launch_step(p, p->steps[i], d_in, d_out, st)) return -1;
+    }
+    if (ev) HIPCHK(hipEventRecord(ev[ns], st));
     return 0;
+}
+
+int pifft_profile_start(pifft_plan* p, int steps) {
+    if (!p || steps < 0) return fail("bad arguments");
+    DeviceGuard g(p->device);
+    const size_t need = (size_t)steps * (p->steps.size() + 1);
+    while (p->prof_ev.size() < need) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        p->prof_ev.push_back(e);
+    }
+    p->prof_steps = steps;
+    p->prof_used = 0;
+    return 0;
+}
+
+int pifft_profile_read(pifft_plan* p, float* launch_ms_sum, int max_launches) {
+    if (!p) return fail("plan is NULL");
+    DeviceGuard g(p->device);
+    const size_t ns = p->steps.size();
+    const int used = p->prof_used;
+    std::vector<float> sum(ns, 0.0f);
+    if (used > 0) HIPCHK(hipEventSynchronize(p->prof_ev[(size_t)used * (ns + 1) - 1]));
+    for (int k = 0; k < used; k++) {
+        hipEvent_t* ev = &p->prof_ev[(size_t)k * (ns + 1)];
+        for (size_t i = 0; i < ns; i++) {
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+            sum[i] += ms;
+        }
+    }
+    if (launch_ms_sum)
+        for (int i = 0; i < max_launches && i < (int)ns; i++) launch_ms_sum[i] = sum[i];
+    p->prof_steps = p->prof_used = 0;
+    return used;
 }
 
 int pifft_execute_device_timed(pifft_plan* p, const void* d_in, void* d_out, void* stream,

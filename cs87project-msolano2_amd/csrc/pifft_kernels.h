@@ -283,7 +283,17 @@ struct PassArgs {
     // x[i + m M], in_bstride = N
     TreeTw tree;
     uint32_t worker;
+    // XCD-aware tile order: blocks b and b+8 run on one XCD (shared L2); with
+    // log_xg = g > 0, 2^g consecutive tiles (adjacent line groups) are given
+    // to blocks of one XCD.  Needs gridDim.x % (8 << g) == 0 (else identity).
+    uint32_t log_xg;
 };
+
+__device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, uint32_t nblocks) {
+    if (log_xg == 0 || (nblocks & ((8u << log_xg) - 1))) return b;
+    const uint32_t xcd = b & 7, slot = b >> 3, gmask = (1u << log_xg) - 1;
+    return ((uint64_t)(slot >> log_xg) << (log_xg + 3)) + ((uint64_t)xcd << log_xg) + (slot & gmask);
+}
 
 template <int R>
 struct PassShape {
@@ -502,7 +512,8 @@ __global__ __launch_bounds__((PassCfg<R, C>::NT),
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     cx<T> v[PassShape<R>::Q];
-    pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x, blockIdx.x);
+    pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x,
+                                           tile_of_block(blockIdx.x, a.log_xg, gridDim.x));
 }
 
 // ---------------------------------------------------------------------------

@@ -75,6 +75,8 @@ _SIGS = {
     "pifft_interleave_device": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                ctypes.c_int, _P]),
     "pifft_tree_device": (ctypes.c_int, [_P, _P, _P, _P]),
+    "pifft_profile_start": (ctypes.c_int, [_P, ctypes.c_int]),
+    "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
 }
 SYMBOLS = tuple(_SIGS)
 
@@ -182,6 +184,18 @@ class Plan:
         _check(lib().pifft_execute_device_timed(self._h, d_in, d_out, _stream(stream), buf, n),
                "pifft_execute_device_timed")
         return list(buf[:n])
+
+    def profile_start(self, steps: int) -> None:
+        _check(lib().pifft_profile_start(self._h, steps), "pifft_profile_start")
+
+    def profile_read(self) -> tuple[int, list[float]]:
+        """(executions recorded, per-launch ms summed over them)."""
+        n = self.info.num_launches
+        buf = (ctypes.c_float * max(n, 1))()
+        used = lib().pifft_profile_read(self._h, buf, n)
+        if used < 0:
+            raise PifftError(f"pifft_profile_read: {last_error()}")
+        return used, list(buf[:n])
 
     def execute(self, host_in, host_out=None):
         """numpy in -> natural-order numpy out (only this plan's bins written)."""

@@ -107,6 +107,16 @@ int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* 
 int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, void* stream,
                                float* launch_ms, int max_launches);
 
+/* Asynchronous per-launch timing: after pifft_profile_start(plan, steps),
+ * each of the next `steps` pifft_execute_device calls records a HIP event
+ * before every launch and after the last one on its stream (no host sync);
+ * pifft_profile_read waits for the last recorded event, writes the per-launch
+ * duration summed over the recorded executions to launch_ms_sum[0 ..
+ * min(num_launches, max_launches)), stops profiling and returns the number of
+ * executions recorded (or -1). */
+int pifft_profile_start(pifft_plan* plan, int steps);
+int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int max_launches);
+
 /* Host boundary, the reference's run() shape: copies host_in (batch*N values)
  * to the device (untimed), runs, and if host_out != NULL writes this plan's
  * bins at their natural-order positions of host_out (batch*N values; other

@@ -224,6 +224,13 @@ def test_timed_execution_reports_every_launch():
     ms = plan.execute_device_timed(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
     assert len(ms) == d["num_launches"] and all(m > 0 for m in ms)
     assert d["launch_kind"][0] == "tree" and d["launch_kind"][-1] == "interleave"
+    # asynchronous profiling: events for 3 back-to-back executions, one read
+    plan.profile_start(3)
+    for _ in range(5):  # only the first 3 are recorded
+        plan.execute_device(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
+    used, sums = plan.profile_read()
+    assert used == 3 and len(sums) == d["num_launches"] and all(m > 0 for m in sums)
+    assert plan.profile_read()[0] == 0
 
 
 def test_device_errors():
