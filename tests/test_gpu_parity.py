@@ -416,3 +416,30 @@ def test_config5_one_worker_of_8_n2e32():
     got = y[kk].cpu().numpy()
     scale = torch.linalg.vector_norm(x).item()
     assert np.max(np.abs(got - want)) <= 1e-10 * scale, (got, want)
+
+
+# ------------------------------------------- the reference's run(), patched ---
+def _ref_gpu(prec):
+    p = os.path.join(oracle.REF_DIR, "fourier-parallel-pi-cpu-pthreads-gpu" + ("-f64" if prec == 64 else ""))
+    if not os.path.exists(p):
+        pytest.skip("oracle/_ref integration binary not built (make -C oracle ref-gpu)")
+    return p
+
+
+@pytest.mark.parametrize("prec", [32, 64])
+def test_reference_run_with_pifft_backend(prec):
+    """INTEGRATION.md section 2 applied to the reference source itself: its own
+    main / setup_from_args / initialize_data / verify_results, with the worker
+    fan-out of run() replaced by pifft_plan_create + pifft_execute."""
+    import subprocess
+    exe = _ref_gpu(prec)
+    for P in ("1", "2", "4", "8"):
+        r = subprocess.run([exe, "-t", "-p", P], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert "Output is correct. Test passed." in r.stdout
+    r = subprocess.run([exe, "-n", "1048576", "-p", "8", "-o"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    cols = r.stdout.strip().split("\t")
+    assert len(cols) == 5 and cols[:2] == ["1048576", "8"]
+    r = subprocess.run([exe, "-n", "1048576"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1 and "Missing option: -p" in r.stderr
