@@ -157,6 +157,7 @@ namespace {
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
+        if (dev < 0) return;  // dry-run plans touch no device
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         if (prev != dev) (void)hipSetDevice(dev);
     }
@@ -231,7 +232,7 @@ struct PassChoice {
 // lines give 256-B contiguous row segments (the HBM-efficient width measured
 // by tools/probe_bw.hip).
 int tile_elems(int prec) {
-    return env_int(prec == 64 ? "PIFFT_TILE64" : "PIFFT_TILE32", prec == 64 ? 8192 : 16384);
+    return env_int(prec == 64 ? "PIFFT_TILE64" : "PIFFT_TILE32", 8192);
 }
 
 int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines, const char* env_c, int mode) {
@@ -261,9 +262,25 @@ int pick_nts(uint64_t pass_bytes) {
     return pass_bytes > (256ull << 20) ? 1 : 0;
 }
 
-// heavy_first: the first pass carries extra reads (the fused tree reads P
-// leaves per input), so it gets the smallest radix -> the widest line group.
-int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, bool heavy_first = false) {
+// HBM rate of a pass side, by the contiguous bytes per row segment (TB/s).
+// Measured on MI355X with tools/probe_bw.hip (strided tile copies) and the
+// pass kernels themselves (profiles/r01_tune_*.log); contiguous ~5.6.
+double seg_rate(double seg_bytes) {
+    if (seg_bytes >= 1024) return 5.6;
+    if (seg_bytes >= 512) return 5.5;
+    if (seg_bytes >= 256) return 5.3;
+    if (seg_bytes >= 128) return 4.2;
+    if (seg_bytes >= 64) return 2.6;
+    return 1.5;
+}
+
+// Local FFT of length M as passes.  A single LDS/register-resident pass when M
+// fits (M <= 2^14); otherwise k Stockham passes with balanced radices, k and
+// the radix order chosen by a bandwidth model: each pass moves its bytes at
+// the rate of its narrowest strided side (C*esz-byte row segments).
+// heavy_first: the first pass also evaluates the tree (reads P leaves per
+// input, P = 2^lp), so its read side dominates.
+int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, int heavy_lp = 0) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
@@ -278,19 +295,40 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         return 0;
     }
     const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32", 10);
-    const int k = (logm + rmax_log - 1) / rmax_log;
-    const int base = logm / k, extra = logm % k;
-    for (int p = 0; p < k; p++) {
-        // larger radices first (the first pass has one contiguous side), or
-        // smallest first when the first pass is the heavy one
-        const int bits = heavy_first ? base + (p >= k - extra ? 1 : 0) : base + (p < extra ? 1 : 0);
-        const int R = 1 << bits;
-        const int mode = p == 0 ? 1 : 2;
-        const int C = pick_lines(prec, R, M >> bits, ntrans * (M >> bits),
-                                 prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
-        if (!find_pass(prec, R, C, mode, nts)) return fail("no pass kernel for R=%d C=%d mode %d", R, C, mode);
-        out.push_back({R, C, mode, nts});
+    const int kmin = (logm + rmax_log - 1) / rmax_log;
+    const int kmax = env_int("PIFFT_PASSES", 0) > 0 ? env_int("PIFFT_PASSES", 0) : kmin + 1;
+    double best = 1e300;
+    // data that stays in the 256 MiB Infinity Cache is not bound by HBM row
+    // segments: fewest passes there
+    const bool resident = 2 * ntrans * M * esz <= (256ull << 20);
+    const int klast = resident && env_int("PIFFT_PASSES", 0) <= 0 ? kmin : kmax;
+    for (int k = env_int("PIFFT_PASSES", 0) > 0 ? kmax : kmin; k <= klast; k++) {
+        if (logm < 4 * k) break;  // every radix >= 16
+        const int base = logm / k, extra = logm % k;
+        for (int order = 0; order < 2; order++) {  // 0: larger radices first, 1: smaller first
+            std::vector<PassChoice> cand;
+            double cost = 0.0;
+            bool ok = true;
+            for (int p = 0; p < k && ok; p++) {
+                const int bits = order ? base + (p >= k - extra ? 1 : 0) : base + (p < extra ? 1 : 0);
+                const int R = 1 << bits;
+                const int mode = p == 0 ? 1 : 2;
+                const int C = pick_lines(prec, R, M >> bits, ntrans * (M >> bits),
+                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
+                if (!find_pass(prec, R, C, mode, nts)) { ok = false; break; }
+                const double rs = seg_rate((double)C * esz);           // strided side
+                const double side = (double)ntrans * M * esz * 1e-12;  // TB per side
+                const double reads = (p == 0 && heavy_lp) ? side * (1 << heavy_lp) : side;
+                cost += reads / rs + side / (mode == 1 ? 5.6 : rs);
+                cand.push_back({R, C, mode, nts});
+            }
+            if (ok && cost < best) {
+                best = cost;
+                out = cand;
+            }
+        }
     }
+    if (out.empty()) return fail("no pass decomposition for M=2^%d", logm);
     return 0;
 }
 
@@ -308,12 +346,13 @@ void release(pifft_plan* p) {
     delete p;
 }
 
-int build_plan(pifft_plan* p) {
+// dry: plan only (pifft_plan_dry_run) -- no device, no allocation
+int build_plan(pifft_plan* p, bool dry = false) {
     const size_t esz = p->esz;
     const uint64_t ntrans = (uint64_t)p->batch * p->nq;  // local transforms
     std::vector<PassChoice> passes;
     const bool may_fuse = p->P > 1 && p->nq == 1 && p->lp <= 4 && env_int("PIFFT_FUSE_TREE", 1);
-    if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse)) return -1;
+    if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0)) return -1;
 
     TableBuilder tb(esz);
     // --- tree tables (w_N) ---
@@ -342,8 +381,10 @@ int build_plan(pifft_plan* p) {
     if (passes.size() > 1) pass2 = two_level(tb, p->m);
     tb.align();
     p->tw_bytes = tb.blob.size() ? tb.blob.size() : 256;
-    HIPCHK(hipMalloc(&p->d_tw, p->tw_bytes));
-    if (!tb.blob.empty()) HIPCHK(hipMemcpy(p->d_tw, tb.blob.data(), tb.blob.size(), hipMemcpyHostToDevice));
+    if (!dry) {
+        HIPCHK(hipMalloc(&p->d_tw, p->tw_bytes));
+        if (!tb.blob.empty()) HIPCHK(hipMemcpy(p->d_tw, tb.blob.data(), tb.blob.size(), hipMemcpyHostToDevice));
+    }
     auto twp = [&](size_t off) { return (const void*)((const char*)p->d_tw + off); };
     TreeTw ttw{};
     if (need_tree) {
@@ -449,7 +490,8 @@ int build_plan(pifft_plan* p) {
         s.grid = dim3((unsigned)wgs);
         s.lds = (size_t)k->lds_bytes;
         s.bytes = fuse_here ? (uint64_t)p->batch * (p->n + M) * esz : 2 * ntrans * M * esz;
-        if (s.lds > 65536) (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
+        if (s.lds > 65536 && !dry)
+            (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {
             p->radix[i] = k->R;
             p->lines[i] = k->C;
@@ -494,6 +536,7 @@ int build_plan(pifft_plan* p) {
     }
     if (p->steps.size() > 4096) return fail("plan too large (%zu launches)", p->steps.size());
     p->bytes_w = need_w ? (size_t)p->batch * p->nq * M * esz : 0;
+    if (dry) return 0;
     if (p->bytes_w) HIPCHK(hipMalloc(&p->buf[BUF_W], p->bytes_w));
     if (p->bytes_ta) HIPCHK(hipMalloc(&p->buf[BUF_TA], p->bytes_ta));
     if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
@@ -504,7 +547,7 @@ int build_plan(pifft_plan* p) {
 }
 
 int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint32_t count,
-           uint32_t batch, int prec, int device, int flags) {
+           uint32_t batch, int prec, int device, int flags, bool dry = false) {
     if (!out) return fail("plan pointer is NULL");
     *out = nullptr;
     if (n < 2 || !is_pow2(n)) return fail("Invalid input size (should be 2^i for i>0)");
@@ -517,9 +560,11 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
     if (flags != PIFFT_OUT_NATURAL && flags != PIFFT_OUT_SLICES) return fail("unknown flags %d", flags);
     if (flags == PIFFT_OUT_NATURAL && count != workers)
         return fail("natural-order output needs all workers on one plan (use PIFFT_OUT_SLICES)");
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail("no HIP device available");
-    if (device < 0 || device >= ndev) return fail("device %d out of range (%d devices)", device, ndev);
+    if (!dry) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail("no HIP device available");
+        if (device < 0 || device >= ndev) return fail("device %d out of range (%d devices)", device, ndev);
+    }
     pifft_plan* p = new pifft_plan;
     p->n = n;
     p->P = workers;
@@ -535,8 +580,9 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
     p->log_n = ilog2u(n);
     p->log_m = p->log_n - p->lp;
     p->m = n >> p->lp;
-    DeviceGuard g(device);
-    if (build_plan(p)) {
+    if (dry) p->device = -1;
+    DeviceGuard g(dry ? -1 : device);
+    if (build_plan(p, dry)) {
         std::string keep = g_err;
         release(p);
         g_err = keep;
@@ -671,6 +717,16 @@ int pifft_plan_create_slices(pifft_plan** plan, uint64_t n, uint32_t workers, ui
 }
 
 void pifft_plan_destroy(pifft_plan* plan) { release(plan); }
+
+int pifft_plan_dry_run(uint64_t n, uint32_t workers, uint32_t first, uint32_t count, uint32_t batch, int prec,
+                       int flags, pifft_plan_info* info) {
+    if (!info) return fail("info is NULL");
+    pifft_plan* p = nullptr;
+    if (create(&p, n, workers, first, count, batch, prec, -1, flags, true)) return -1;
+    const int rc = pifft_plan_get_info(p, info);
+    release(p);
+    return rc;
+}
 
 int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     if (!p || !info) return fail("NULL argument");

@@ -295,19 +295,24 @@ __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, u
     return ((uint64_t)(slot >> log_xg) << (log_xg + 3)) + ((uint64_t)xcd << log_xg) + (slot & gmask);
 }
 
-template <int R>
+// values held per thread (VPT).  16 for both precisions: 32 fp32 values (the
+// same bytes as 16 fp64) measured 160-200 VGPRs with spills at 128.
+template <typename T>
+constexpr int vpt_of() { return 16; }  // 32 for fp32 measured: 160-200 VGPRs, spills
+
+template <int R, int VPT = 16>
 struct PassShape {
-    static constexpr int Q = R >= 16 ? 16 : R;              // values per thread
+    static constexpr int Q = R >= VPT ? VPT : (R >= 16 ? 16 : R);  // values per thread
     static constexpr int LOGR = ilog2c(R);
     static constexpr int NSTG = (LOGR + 3) / 4;              // radix-16 stages + 1 trailing
     static constexpr int QL = 1 << (LOGR - 4 * (NSTG - 1));  // trailing radix 2/4/8/16
     static constexpr int LS = R + R / 16 + 1;                // LDS line stride (odd, scalars)
 };
 
-template <int R, int C>
+template <int R, int C, int VPT = 16>
 struct PassCfg {
-    static constexpr int NT = C * R / PassShape<R>::Q;
-    static constexpr int lds_elems = PassShape<R>::NSTG > 1 ? C * PassShape<R>::LS : 0;  // scalars
+    static constexpr int NT = C * R / PassShape<R, VPT>::Q;
+    static constexpr int lds_elems = PassShape<R, VPT>::NSTG > 1 ? C * PassShape<R, VPT>::LS : 0;  // scalars
 #ifndef PIFFT_MIN_WG_PER_CU
 #define PIFFT_MIN_WG_PER_CU 2
 #endif
@@ -333,15 +338,15 @@ __device__ __forceinline__ void apply_powers(cx<T>* v, const cx<T>* anc) {
 }
 
 // Stage S of the R-point sub-FFT in a pass of mode MODE:
-//   radix q (16, the last one 2/4/8/16), U = 16/q butterflies per thread,
+//   radix q (16, the last one 2/4/8/16), U = Q/q butterflies per thread,
 //   NB = R/q butterflies per line, ns = 16^S (product of previous radices).
 // Butterfly g = tid + u*NT maps to (line c, butterfly b) "c-fast" (lanes
 // across lines: the strided side of a pass in HBM) or "b-fast" (lanes along
 // a line: LDS stages and contiguous HBM sides).
-template <int R, int C, int MODE, int S>
+template <int R, int C, int MODE, int S, int VPT>
 struct Stage {
-    using Sh = PassShape<R>;
-    static constexpr int NT = PassCfg<R, C>::NT;
+    using Sh = PassShape<R, VPT>;
+    static constexpr int NT = PassCfg<R, C, VPT>::NT;
     static constexpr bool first = S == 0, last = S == Sh::NSTG - 1;
     static constexpr int q = last ? Sh::QL : 16;
     static constexpr int U = Sh::Q / q;
@@ -358,8 +363,9 @@ struct Stage {
 template <typename T, int R, int C, int MODE, bool NTS, int LP, int S>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
-    using St = Stage<R, C, MODE, S>;
-    using Sh = PassShape<R>;
+    constexpr int VPT = vpt_of<T>();
+    using St = Stage<R, C, MODE, S, VPT>;
+    using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns, LS = Sh::LS;
     const uint64_t lb_mask = (1ull << a.log_lb) - 1;
     const uint64_t ns_mask = (1ull << a.log_ns) - 1;
@@ -472,7 +478,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         }
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
-        using Nx = Stage<R, C, MODE, S + 1>;
+        using Nx = Stage<R, C, MODE, S + 1, VPT>;
 #pragma unroll
         for (int comp = 0; comp < 2; comp++) {
             __syncthreads();
@@ -507,11 +513,13 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // NTS: non-temporal streaming of the data (see ld_stream)
 template <typename T, int R, int C, int MODE, bool NTS, int LP>
-__global__ __launch_bounds__((PassCfg<R, C>::NT),
-                             (MODE == 3 && LP >= 4 && PassCfg<R, C>::waves_per_eu > 2 ? 2 : PassCfg<R, C>::waves_per_eu))
+__global__ __launch_bounds__((PassCfg<R, C, vpt_of<T>()>::NT),
+                             (MODE == 3 && LP >= 4 && PassCfg<R, C, vpt_of<T>()>::waves_per_eu > 2
+                                  ? 2
+                                  : PassCfg<R, C, vpt_of<T>()>::waves_per_eu))
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
-    cx<T> v[PassShape<R>::Q];
+    cx<T> v[PassShape<R, vpt_of<T>()>::Q];
     pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x,
                                            tile_of_block(blockIdx.x, a.log_xg, gridDim.x));
 }

@@ -62,6 +62,8 @@ _SIGS = {
                                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "pifft_plan_destroy": (None, [_P]),
+    "pifft_plan_dry_run": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.POINTER(PlanInfo)]),
     "pifft_plan_get_info": (ctypes.c_int, [_P, ctypes.POINTER(PlanInfo)]),
     "pifft_execute_device": (ctypes.c_int, [_P, _P, _P, _P]),
     "pifft_execute_device_timed": (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_float),
@@ -163,17 +165,7 @@ class Plan:
         return self._h
 
     def describe(self) -> dict:
-        i = self.info
-        nl = i.num_launches
-        return {
-            "n": i.n, "workers": i.workers, "first_worker": i.first_worker, "num_workers": i.num_workers,
-            "batch": i.batch, "prec": i.prec, "local_n": i.local_n, "in_elems": i.in_elems,
-            "out_elems": i.out_elems, "workspace_bytes": i.workspace_bytes, "num_launches": nl,
-            "num_passes": i.num_passes, "tree_launches": i.tree_launches,
-            "radix": list(i.radix[: i.num_passes]), "lines": list(i.lines[: i.num_passes]),
-            "launch_bytes": list(i.launch_bytes[: min(nl, 64)]),
-            "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, 64)]],
-        }
+        return describe_info(self.info)
 
     def execute_device(self, d_in: int, d_out: int, stream=None) -> None:
         _check(lib().pifft_execute_device(self._h, d_in, d_out, _stream(stream)), "pifft_execute_device")
@@ -220,6 +212,31 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+def describe_info(i: PlanInfo) -> dict:
+    nl = i.num_launches
+    return {
+        "n": i.n, "workers": i.workers, "first_worker": i.first_worker, "num_workers": i.num_workers,
+        "batch": i.batch, "prec": i.prec, "local_n": i.local_n, "in_elems": i.in_elems,
+        "out_elems": i.out_elems, "workspace_bytes": i.workspace_bytes, "num_launches": nl,
+        "num_passes": i.num_passes, "tree_launches": i.tree_launches,
+        "radix": list(i.radix[: i.num_passes]), "lines": list(i.lines[: i.num_passes]),
+        "launch_bytes": list(i.launch_bytes[: min(nl, 64)]),
+        "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, 64)]],
+    }
+
+
+def dry_run(n: int, workers: int = 1, batch: int = 1, prec: int = F64, *, first: int = 0,
+            count: int | None = None, flags: int | None = None) -> dict:
+    """The plan that would be built, without a device (host planning only)."""
+    count = workers if count is None else count
+    if flags is None:
+        flags = OUT_NATURAL if count == workers else OUT_SLICES
+    info = PlanInfo()
+    _check(lib().pifft_plan_dry_run(n, workers, first, count, batch, prec, flags, ctypes.byref(info)),
+           "pifft_plan_dry_run")
+    return describe_info(info)
 
 
 def execute_group(plans, host_in, host_out=None):

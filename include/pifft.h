@@ -94,6 +94,11 @@ int pifft_plan_create_slices(pifft_plan** plan, uint64_t n, uint32_t workers, ui
 
 void pifft_plan_destroy(pifft_plan* plan);
 
+/* The plan pifft_plan_create_slices would build, described without touching
+ * a device or allocating (host-side planning only; device = -1 in info). */
+int pifft_plan_dry_run(uint64_t n, uint32_t workers, uint32_t first, uint32_t count, uint32_t batch,
+                       int prec, int flags, pifft_plan_info* info);
+
 int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
 
 /* Device boundary: d_in holds info.in_elems complex values, d_out receives

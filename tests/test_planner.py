@@ -1,0 +1,71 @@
+"""Host-side planning (pifft_plan_dry_run: no device needed) for the
+BASELINE.json configurations and the edge cases -- the launch structure the
+GPU tests then execute."""
+import pytest
+
+import pifft
+
+F64, F32 = pifft.F64, pifft.F32
+GiB = 1 << 30
+
+
+def test_config1_2e20_fp64_one_worker():
+    d = pifft.dry_run(1 << 20, 1, 1, F64)
+    assert d["launch_kind"] == ["pass"] * d["num_passes"] and d["num_passes"] == 2
+    assert d["radix"] == [1024, 1024]
+
+
+def test_config2_2e20_fp64_eight_workers_one_gpu():
+    d = pifft.dry_run(1 << 20, 8, 1, F64)
+    assert d["launch_kind"][0] == "tree" and d["launch_kind"][-1] == "interleave"
+    assert d["local_n"] == 1 << 17 and d["out_elems"] == 1 << 20
+
+
+def test_config3_batched_fp32_single_pass():
+    d = pifft.dry_run(4096, 1, 4096, F32)
+    assert d["launch_kind"] == ["pass"] and d["radix"] == [4096]
+    assert d["launch_bytes"] == [2 * 4096 * 4096 * 8]
+
+
+def test_config4_2e28_fp64():
+    d = pifft.dry_run(1 << 28, 1, 1, F64)
+    assert d["radix"] == [1024, 512, 512] and d["lines"] == [8, 16, 16]
+    assert d["launch_bytes"] == [2 * (1 << 28) * 16] * 3
+    assert d["workspace_bytes"] >= 4 * GiB
+
+
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+def test_config4_split_fuses_the_tree(P):
+    d = pifft.dry_run(1 << 28, P, 1, F64, first=P - 1, count=1)
+    assert d["launch_kind"][0] == "tree+pass" and "tree" not in d["launch_kind"]
+    assert d["local_n"] == (1 << 28) // P and d["out_elems"] == (1 << 28) // P
+    # the fused pass reads the whole input replica once and writes the worker's N/P
+    assert d["launch_bytes"][0] == ((1 << 28) + (1 << 28) // P) * 16
+    # heavy first pass: smallest radix first (widest row segments)
+    assert d["radix"][0] == min(d["radix"])
+
+
+def test_config5_2e32_one_worker_of_8():
+    d = pifft.dry_run(1 << 32, 8, 1, F64, first=5, count=1)
+    assert d["local_n"] == 1 << 29 and d["launch_kind"][0] == "tree+pass"
+    assert d["launch_bytes"][0] == ((1 << 32) + (1 << 29)) * 16
+
+
+def test_fp32_large_prefers_wide_segments():
+    d = pifft.dry_run(1 << 28, 1, 1, F32)
+    assert all(c * 8 >= 256 for c in d["lines"])  # >= 256-B row segments on every strided side
+
+
+@pytest.mark.parametrize("n,P,kinds", [
+    (2, 1, ["pass"]), (2, 2, ["tree", "interleave"]), (16, 16, ["tree", "interleave"]),
+    (256, 256, ["tree", "tree", "interleave"]), (1 << 16, 32, ["tree", "tree", "pass", "interleave"]),
+])
+def test_edge_plans(n, P, kinds):
+    assert pifft.dry_run(n, P, 1, F64)["launch_kind"] == kinds
+
+
+def test_dry_run_validation():
+    with pytest.raises(pifft.PifftError, match="More processors than inputs"):
+        pifft.dry_run(8, 16)
+    with pytest.raises(pifft.PifftError, match="worker range"):
+        pifft.dry_run(64, 8, first=3, count=2)
