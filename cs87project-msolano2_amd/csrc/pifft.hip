@@ -13,6 +13,9 @@
 // Twiddles are host-built tables in HBM (w_R per pass, two-level w_M and w_N;
 // the tree uses the reference's own omega(N,k) formula up to N = 2^22 so that
 // its output is bit-identical to the reference's post-tree segment).
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE  // sincos (reference_omega)
+#endif
 #include "pifft_kernels.h"
 #include "pifft_table.h"
 #include "../../include/pifft.h"
@@ -202,8 +205,16 @@ struct TableBuilder {
     // omega(N,k), k < count, with the reference's own formula (CPU.c:644-651)
     size_t reference_omega(uint64_t N, uint64_t count) {
         size_t off = align();
-        for (uint64_t k = 0; k < count; k++)
-            put(cos(2.0 * M_PI / (double)N * (double)k), -sin(2.0 * M_PI / (double)N * (double)k));
+        // gcc -O1 and up folds the reference's cos()/sin() pair into one glibc
+        // sincos() call; glibc's sincos and its separate cos/sin disagree in
+        // the last fp64 bit for ~1e-3 of the angles (43 of 2^15 at N=2^16).
+        // The reference build the fixtures pin (-O2) is the sincos one, so the
+        // table is built the same way (clang keeps the pair separate).
+        for (uint64_t k = 0; k < count; k++) {
+            double s, c;
+            sincos(2.0 * M_PI / (double)N * (double)k, &s, &c);
+            put(c, -s);
+        }
         return off;
     }
 };

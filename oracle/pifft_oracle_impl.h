@@ -45,11 +45,18 @@ static inline CX FN(mul)(CX a, CX b) {
 }
 
 /* CPU.c:644-651: omega(N,k) = (cos(2.0*M_PI/N*k), -sin(2.0*M_PI/N*k)), the
- * argument evaluated in double exactly as ((2.0*M_PI)/N)*k, rounded to REAL. */
+ * argument evaluated in double exactly as ((2.0*M_PI)/N)*k, rounded to REAL.
+ * gcc at -O1 and up compiles the reference's cos()/sin() pair into ONE glibc
+ * sincos() call, and glibc's sincos differs from its separate cos/sin in the
+ * last fp64 bit for ~0.1% of angles.  The pinned reference build (-O2, the
+ * fixtures) is the sincos one, so it is spelled out here rather than left to
+ * the optimiser (an -O0 build of this file would otherwise drift). */
 CX FN(omega)(uint64_t N, uint64_t k) {
     CX o;
-    o.re = cos(2.0 * M_PI / (double)N * (double)k);
-    o.im = -sin(2.0 * M_PI / (double)N * (double)k);
+    double s, c;
+    sincos(2.0 * M_PI / (double)N * (double)k, &s, &c);
+    o.re = c;
+    o.im = -s;
     return o;
 }
 

@@ -10,10 +10,15 @@ script feeds it synthetic inputs (splitmix64, oracle.generate) and stores
   tree_{f32,f64}_n{N}_p{P}.npz  every worker's segment after the tree stage
   manifest.json            sizes, seeds, SHA-256 of the reference outputs
                            (incl. N=2^20 for P=1 and P=8), rel-L2 vs a float64
-                           numpy FFT
+                           numpy FFT, and per-worker SHA-256 of the post-tree
+                           segments at N=2^16..2^20 ("tree_big": sizes where
+                           glibc's sincos -- what gcc -O2 makes of the
+                           reference's cos/sin pair -- and separate cos/sin
+                           differ on hundreds of fp64 twiddles)
 
 The fixtures are data (inputs and reference outputs), never reference source.
-Re-run:  python tests/golden/gen_golden.py
+Re-run:  python tests/golden/gen_golden.py            (everything)
+         python tests/golden/gen_golden.py tree-big   (only manifest["tree_big"])
 """
 from __future__ import annotations
 
@@ -34,6 +39,7 @@ SEED = 0x5EED
 FFT_SIZES = [2, 4, 8, 16, 64, 1024, 4096]
 TREE_CASES = [(64, 8), (64, 2), (1024, 4), (4096, 16), (256, 256)]
 BIG = 1 << 20
+TREE_BIG = [(1 << 16, 8), (1 << 18, 16), (1 << 20, 4)]
 DT = {"f32": np.complex64, "f64": np.complex128}
 
 
@@ -47,7 +53,27 @@ def rel_l2(a, b) -> float:
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
+def tree_big() -> dict:
+    out = {}
+    for suf, dt in DT.items():
+        for n, P in TREE_BIG:
+            x = oracle.generate(n, dt, SEED)
+            out[f"{suf}_n{n}_p{P}"] = {
+                "n": n, "P": P,
+                "sha256_seg_q": [sha(oracle.run_reference_harness("tree", x, P, q)) for q in range(P)]}
+    return out
+
+
 def main() -> None:
+    if sys.argv[1:] == ["tree-big"]:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "all", "ref"], check=True,
+                       stdout=subprocess.DEVNULL)
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            man = json.load(f)
+        man["tree_big"] = tree_big()
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(man, f, indent=1, sort_keys=True)
+        return
     subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "all", "ref"], check=True,
                    stdout=subprocess.DEVNULL)
     man = {"seed": SEED, "generator": "splitmix64; re,im=(2u-1)/sqrt(N), u=(z>>11)*2^-53, draws 2e,2e+1",
@@ -82,6 +108,7 @@ def main() -> None:
                 big["rel_l2_vs_numpy_f64"] = rel_l2(o, np.fft.fft(x.astype(np.complex128)))
         man["big"][suf] = big
         print(suf, "done", flush=True)
+    man["tree_big"] = tree_big()
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
 

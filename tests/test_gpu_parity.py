@@ -104,6 +104,35 @@ def test_tree_stage_bitwise_vs_reference(suf, n, P):
 
 
 @pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("logn,P", [(12, 2), (16, 8), (18, 16), (20, 4), (22, 32)])
+def test_tree_stage_bitwise_every_worker(suf, logn, P):
+    """Every worker's tree output == the oracle's, bit for bit, at sizes where
+    glibc's sincos and cos/sin disagree on hundreds of fp64 twiddles (the
+    pinned -O2 reference build uses sincos; see oracle/pifft_oracle_impl.h).
+    P = 32 takes two tree launches."""
+    n = 1 << logn
+    x = oracle.generate(n, DT[suf])
+    d_in = dev(x)
+    want = np.concatenate([oracle.tree_segment(x, P, q) for q in range(P)])
+    plan = pifft.Plan(n, P, 1, PREC[suf], first=0, count=P, device=0, flags=pifft.OUT_SLICES)
+    d_all = torch.empty(n, dtype=d_in.dtype, device="cuda")
+    plan.tree_device(d_in.data_ptr(), d_all.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert d_all.cpu().numpy().tobytes() == want.tobytes()
+    m = n // P
+    for q in range(P):
+        p1 = pifft.Plan(n, P, 1, PREC[suf], first=q, count=1, device=0)
+        d1 = torch.empty(m, dtype=d_in.dtype, device="cuda")
+        p1.tree_device(d_in.data_ptr(), d1.data_ptr(), torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert d1.cpu().numpy().tobytes() == want[q * m:(q + 1) * m].tobytes(), f"q={q}"
+    ref = manifest()["tree_big"].get(f"{suf}_n{n}_p{P}")
+    if ref:  # the reference's own per-worker digests
+        got = d_all.cpu().numpy().reshape(P, m)
+        assert [hashlib.sha256(got[q].tobytes()).hexdigest() for q in range(P)] == ref["sha256_seg_q"]
+
+
+@pytest.mark.parametrize("suf", list(DT))
 def test_generator_bitwise(suf):
     n = 1 << 16
     d = torch.empty(n, dtype=TDT[DT[suf]], device="cuda")

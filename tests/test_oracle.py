@@ -97,3 +97,18 @@ def test_worker_owns_stride_p_bins():
         mask[r::P] = True
         assert np.array_equal(part[mask], full[mask])
         assert not np.any(part[~mask])
+
+
+@pytest.mark.parametrize("suf", list(SUFS))
+def test_oracle_tree_big_digests(suf):
+    """Post-tree segments at N=2^16..2^20, every worker, == the reference's
+    (SHA-256 per worker, manifest["tree_big"]).  At these sizes glibc's sincos
+    (what gcc -O2 makes of the reference's cos/sin pair, CPU.c:647-648) and a
+    separate cos/sin differ on hundreds of fp64 twiddles, so this pins the
+    oracle's omega to the -O2 reference build."""
+    for key, case in manifest()["tree_big"].items():
+        if not key.startswith(suf):
+            continue
+        x = oracle.generate(case["n"], SUFS[suf], manifest()["seed"])
+        for q, want in enumerate(case["sha256_seg_q"]):
+            assert _sha(oracle.tree_segment(x, case["P"], q)) == want, f"{key} q={q}"
