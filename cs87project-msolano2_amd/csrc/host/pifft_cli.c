@@ -11,7 +11,7 @@
  *            show_usage, print_input/print_output, verify_results (CPU.c:293-302, 659-705)
  *
  *   pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b batch] [-s seed] [-g gpus]
- *         [-w file] [-x] [-W warmups] [-l]
+ *         [-w file] [-r] [-x] [-W warmups] [-l]
  *
  * Output: the reference's 5-column TSV "n p total stage1 stage2" in ms
  * (CPU.c:485-492), once.  stage 1 = tree, stage 2 = local FFT (+ reorder).
@@ -20,7 +20,9 @@
  * Extensions: -f precision (default 32 = the reference's data_t), -b batch of
  * independent transforms, -s seed (default: hash of the time, as CPU.c:244),
  * -g number of GPUs the P workers are spread over (default 1), -w dump the
- * natural-order output (binary), -x extra columns (GFLOP/s, GB/s),
+ * natural-order output (binary), -r keep the output in the reference's own
+ * scratch order (bit-reversed, tmp_in before CPU.c:496-499's scatter; no
+ * reorder launch), -x extra columns (GFLOP/s, GB/s),
  * -W untimed warm-up runs before the timed one (default 1; code-object load),
  * -l list GPUs (the how-many-* utilities).  -n is parsed as 64-bit.
  */
@@ -53,12 +55,13 @@ typedef struct tr {
     const char* dump;    /* -w */
     int extra;           /* -x */
     int warmups;         /* -W */
+    int bitrev;          /* -r */
 } tr_t;
 
 static void show_usage(void) {
     print_out("\nusage:\n"
               "  pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b <batch>] [-s <seed>]\n"
-              "        [-g <gpus>] [-w <file>] [-x] [-W <warmups>] [-l]\n"
+              "        [-g <gpus>] [-w <file>] [-r] [-x] [-W <warmups>] [-l]\n"
               "\noptions:\n"
               "  -n <n>     power of two input size\n"
               "  -p <p>     power of two number of processors (less than n)\n"
@@ -68,7 +71,8 @@ static void show_usage(void) {
               "  -b <b>     batch of independent transforms (default 1)\n"
               "  -s <seed>  input seed (default: hash of the time)\n"
               "  -g <g>     GPUs to spread the p workers over (default 1)\n"
-              "  -w <file>  write the natural-order output (binary data_t)\n"
+              "  -w <file>  write the output (binary data_t; natural order unless -r)\n"
+              "  -r         output in the reference's bit-reversed scratch order\n"
               "  -x         extra columns: GFLOP/s, algorithmic GB/s\n"
               "  -W <w>     untimed warm-up runs (default 1)\n"
               "  -l         list GPUs and exit\n"
@@ -107,7 +111,7 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
     t->batch = 1;
     t->gpus = 1;
     t->warmups = 1;
-    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:xW:l")) != -1) {
+    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:rxW:l")) != -1) {
         switch (ret) {
             case 'n':
                 if (parse_u64(optarg, &num) || !(num > 1) || !is_power_of_two_u64(num)) {
@@ -165,6 +169,9 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
                 break;
             case 'w':
                 t->dump = optarg;
+                break;
+            case 'r':
+                t->bitrev = 1;
                 break;
             case 'x':
                 t->extra = 1;
@@ -265,8 +272,10 @@ static void print_output(const tr_t* t) {
 /* CPU.c:689-705 */
 static void verify_results(const tr_t* t) {
     static const double want[8] = {4, 0, 0, 0, -4, 0, 0, 0};
+    static const double want_brev[8] = {4, -4, 0, 0, 0, 0, 0, 0};  /* tmp_in order */
     int ok = t->N >= 8;
-    for (int i = 0; ok && i < 8; i++) ok = re_at(t, t->out, i) == want[i] && im_at(t, t->out, i) == 0.0;
+    const double* w = t->bitrev ? want_brev : want;
+    for (int i = 0; ok && i < 8; i++) ok = re_at(t, t->out, i) == w[i] && im_at(t, t->out, i) == 0.0;
     print_out(ok ? "Output is correct. Test passed.\n\n" : "Output is incorrect! Test failed.\n\n");
 }
 
@@ -314,9 +323,9 @@ int run(tr_t* t) {
     if (initialize_data(t)) goto done;
     for (uint32_t g = 0; g < G; g++) {
         int r = (G == 1) ? pifft_plan_create_slices(&plans[g], t->N, t->P, 0, t->P, t->batch, t->prec, 0,
-                                                    PIFFT_OUT_NATURAL)
+                                                    t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_NATURAL)
                          : pifft_plan_create_slices(&plans[g], t->N, t->P, g * per, per, t->batch, t->prec,
-                                                    (int)g, PIFFT_OUT_SLICES);
+                                                    (int)g, t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_SLICES);
         if (r) {
             stderr_out("(GPU %u): %s\n", g, pifft_last_error());
             goto done;

@@ -84,14 +84,17 @@ PIFFT_DECL_PART(2)
 PIFFT_DECL_PART(3)
 PIFFT_DECL_PART(4)
 PIFFT_DECL_PART(5)
+PIFFT_DECL_PART(6)
+PIFFT_DECL_PART(7)
 namespace {
-static_assert(PIFFT_NPART == 6, "update the part list");
+static_assert(PIFFT_NPART == 8, "update the part list");
 
 const std::vector<PassKernel>& pass_kernels() {
     static const std::vector<PassKernel> all = [] {
         std::vector<PassKernel> v;
         const PassKernel* (*parts[])(int*) = {pifft_pass_table_0, pifft_pass_table_1, pifft_pass_table_2,
-                                               pifft_pass_table_3, pifft_pass_table_4, pifft_pass_table_5};
+                                               pifft_pass_table_3, pifft_pass_table_4, pifft_pass_table_5,
+                                               pifft_pass_table_6, pifft_pass_table_7};
         for (auto f : parts) {
             int n = 0;
             const PassKernel* t = f(&n);
@@ -137,6 +140,7 @@ struct pifft_plan {
     int lp = 0, log_n = 0, log_m = 0;
     size_t esz = 16;
     bool natural = true;
+    bool bitrev = false;  // PIFFT_OUT_BITREV
     std::vector<Step> steps;
     int tree_steps = 0, npasses = 0;
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
@@ -364,6 +368,18 @@ int build_plan(pifft_plan* p, bool dry = false) {
     std::vector<PassChoice> passes;
     const bool may_fuse = p->P > 1 && p->nq == 1 && p->lp <= 4 && env_int("PIFFT_FUSE_TREE", 1);
     if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0)) return -1;
+    if (p->bitrev && !passes.empty()) {
+        // the last pass stores in bit-reversed order: its MODE | 4 twin, at
+        // the planned C or the widest instantiated one below it
+        PassChoice& l = passes.back();
+        const int bm = l.mode, cmin = bm == 0 ? 1 : 4;
+        int C = l.C;
+        while (C > cmin && !find_pass(p->prec, l.R, C, bm | 4, l.nts)) C /= 2;
+        if (!find_pass(p->prec, l.R, C, bm | 4, l.nts))
+            return fail("no bit-reversed pass kernel R=%d C=%d mode=%d", l.R, l.C, bm);
+        l.C = C;
+        l.mode = bm | 4;
+    }
 
     TableBuilder tb(esz);
     // --- tree tables (w_N) ---
@@ -493,7 +509,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.log_lb = (uint32_t)(p->log_m - logr);
         s.pa.log_ns = (uint32_t)ilog2u(ns);
         s.pa.tw_shift = (uint32_t)(p->log_m - ilog2u(ns) - logr);
-        s.pa.log_xg = (uint32_t)env_int(passes[i].mode == 0 ? "PIFFT_XCD_GROUP_SINGLE" : "PIFFT_XCD_GROUP", passes[i].mode == 0 ? 0 : 2);
+        s.pa.log_xg = (uint32_t)env_int((passes[i].mode & 3) == 0 ? "PIFFT_XCD_GROUP_SINGLE" : "PIFFT_XCD_GROUP",
+                                        (passes[i].mode & 3) == 0 ? 0 : 2);
         s.block = dim3((unsigned)k->nt);
         const uint64_t wgs = (s.pa.nlines + k->C - 1) / k->C;
         if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
@@ -568,7 +585,8 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
         return fail("invalid worker range [%u, %u) of %u", first, first + count, workers);
     if (batch == 0) return fail("batch must be >= 1");
     if (prec != PIFFT_F32 && prec != PIFFT_F64) return fail("prec must be PIFFT_F32 or PIFFT_F64");
-    if (flags != PIFFT_OUT_NATURAL && flags != PIFFT_OUT_SLICES) return fail("unknown flags %d", flags);
+    if (flags != PIFFT_OUT_NATURAL && flags != PIFFT_OUT_SLICES && flags != PIFFT_OUT_BITREV)
+        return fail("unknown flags %d", flags);
     if (flags == PIFFT_OUT_NATURAL && count != workers)
         return fail("natural-order output needs all workers on one plan (use PIFFT_OUT_SLICES)");
     if (!dry) {
@@ -586,6 +604,7 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
     p->device = device;
     p->flags = flags;
     p->natural = (flags == PIFFT_OUT_NATURAL);
+    p->bitrev = (flags == PIFFT_OUT_BITREV);
     p->esz = prec == PIFFT_F64 ? 16 : 8;
     p->lp = ilog2u(workers);
     p->log_n = ilog2u(n);
@@ -681,6 +700,12 @@ void scatter_to_host(const pifft_plan* p, const char* res, char* host_out) {
         return;
     }
     const uint64_t M = p->m;
+    if (p->bitrev) {  // the reference's tmp_in layout: segments at q M
+        for (uint32_t bt = 0; bt < p->batch; bt++)
+            memcpy(host_out + ((uint64_t)bt * p->n + (uint64_t)p->q0 * M) * esz,
+                   res + (uint64_t)bt * p->nq * M * esz, (size_t)p->nq * M * esz);
+        return;
+    }
     for (uint32_t bt = 0; bt < p->batch; bt++) {
         for (uint32_t q = p->q0; q < p->q0 + p->nq; q++) {
             const uint64_t r = bitrev(q, p->lp);

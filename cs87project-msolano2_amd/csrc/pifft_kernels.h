@@ -364,12 +364,39 @@ template <typename T, int R, int C, int MODE, bool NTS, int LP, int S>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
     constexpr int VPT = vpt_of<T>();
-    using St = Stage<R, C, MODE, S, VPT>;
+    // MODE | 4: the same pass storing at bitrev_{log2 M}(natural position),
+    // the reference's scratch order (PIFFT_OUT_BITREV; last pass only).  Each
+    // line's R outputs still land in one contiguous R-element block; plain
+    // (L2-merged) stores.  A compile-time variant: a run-time flag in the
+    // store path cost 5-15 % on every pass (tools/ab.sh).
+    constexpr int BM = MODE & 3;
+    constexpr bool BREV = (MODE & 4) != 0;
+    using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns, LS = Sh::LS;
     const uint64_t lb_mask = (1ull << a.log_lb) - 1;
     const uint64_t ns_mask = (1ull << a.log_ns) - 1;
 
+    // MODE 2: the inter-pass twiddle factors depend only on (line, b); their
+    // two-level table entries are fetched with the data, not after it (a
+    // second dependent round trip per workgroup otherwise)
+    [[maybe_unused]] C2 tw_pre[St::first && BM == 2 ? 4 * U : 1];
+    if constexpr (St::first && BM == 2) {
+        const C2* tlo = static_cast<const C2*>(a.tw_lo);
+        const C2* thi = static_cast<const C2*>(a.tw_hi);
+        const uint64_t hmask = (1ull << a.tw_h) - 1;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            int c, b;
+            St::map(tid, u, c, b);
+            const uint64_t jm = ((tile * C + c) & lb_mask) & ns_mask;
+            const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
+            tw_pre[4 * u + 0] = tlo[e0 & hmask];
+            tw_pre[4 * u + 1] = thi[e0 >> a.tw_h];
+            tw_pre[4 * u + 2] = tlo[e1 & hmask];
+            tw_pre[4 * u + 3] = thi[e1 >> a.tw_h];
+        }
+    }
     if constexpr (St::first) {
         // ---- inputs straight from HBM (all loads issued before any use) ----
         const C2* __restrict__ in = static_cast<const C2*>(a.in);
@@ -381,7 +408,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const bool ok = line < a.nlines;
             const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
             const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.log_lb);
-            if constexpr (MODE == 3) {
+            if constexpr (BM == 3) {
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
                 // to P = 8 at 128 VGPRs
@@ -413,18 +440,13 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         }
     }
     // ---- twiddles before the butterflies ----
-    if constexpr (St::first && MODE == 2) {
+    if constexpr (St::first && BM == 2) {
         // w_{Ns R}^{(j mod Ns) r}, r = b + k NB: the k-dependent factor
         // step^k now, the common factor w^{(j mod Ns) b} after the DFT
-        const C2* tlo = static_cast<const C2*>(a.tw_lo);
-        const C2* thi = static_cast<const C2*>(a.tw_hi);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            int c, b;
-            St::map(tid, u, c, b);
-            const uint64_t jm = ((tile * C + c) & lb_mask) & ns_mask;
             C2 anc[4];
-            anc[0] = tw2(tlo, thi, a.tw_h, (jm * (uint64_t)NB) << a.tw_shift);
+            anc[0] = cmul(tw_pre[4 * u + 1], tw_pre[4 * u + 0]);  // = tw2(lo, hi, h, jm NB)
 #pragma unroll
             for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
             apply_powers<q>(&v[u * q], anc);
@@ -446,15 +468,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     }
 #pragma unroll
     for (int u = 0; u < U; u++) dft<q>(&v[u * q]);
-    if constexpr (St::first && MODE == 2) {
-        const C2* tlo = static_cast<const C2*>(a.tw_lo);
-        const C2* thi = static_cast<const C2*>(a.tw_hi);
+    if constexpr (St::first && BM == 2) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            int c, b;
-            St::map(tid, u, c, b);
-            const uint64_t jm = ((tile * C + c) & lb_mask) & ns_mask;
-            const C2 base = tw2(tlo, thi, a.tw_h, (jm * (uint64_t)b) << a.tw_shift);
+            const C2 base = cmul(tw_pre[4 * u + 3], tw_pre[4 * u + 2]);  // = tw2(lo, hi, h, jm b)
 #pragma unroll
             for (int k = 0; k < q; k++) v[u * q + k] = cmul(v[u * q + k], base);
         }
@@ -470,15 +487,24 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
                 const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
-                C2* dst = out + bt * a.out_bstride + ((j >> a.log_ns) << (a.log_ns + Sh::LOGR)) + (j & ns_mask) +
-                          ((uint64_t)b << a.log_ns);
+                const uint64_t pos = ((j >> a.log_ns) << (a.log_ns + Sh::LOGR)) + (j & ns_mask) + ((uint64_t)b << a.log_ns);
+                C2* dst = out + bt * a.out_bstride;
+                if constexpr (BREV) {
+                    const uint32_t sh = 64 - (a.log_lb + Sh::LOGR);  // log2 M bits
 #pragma unroll
-                for (int k = 0; k < q; k++) st_stream<NTS>(dst + ((uint64_t)(k * NB) << a.log_ns), v[u * q + k]);
+                    for (int k = 0; k < q; k++) {
+                        const uint64_t pk = pos + ((uint64_t)(k * NB) << a.log_ns);
+                        dst[sh < 64 ? __builtin_bitreverse64(pk) >> sh : 0] = v[u * q + k];
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < q; k++) st_stream<NTS>(dst + pos + ((uint64_t)(k * NB) << a.log_ns), v[u * q + k]);
+                }
             }
         }
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
-        using Nx = Stage<R, C, MODE, S + 1, VPT>;
+        using Nx = Stage<R, C, BM, S + 1, VPT>;
 #pragma unroll
         for (int comp = 0; comp < 2; comp++) {
             __syncthreads();
@@ -511,6 +537,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 // MODE 2: later pass (strided in and out, inter-pass twiddle)
 // MODE 3: first pass with the tree stage fused in (one worker, P = 2^LP):
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
+// MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
 // NTS: non-temporal streaming of the data (see ld_stream)
 template <typename T, int R, int C, int MODE, bool NTS, int LP>
 __global__ __launch_bounds__((PassCfg<R, C, vpt_of<T>()>::NT),

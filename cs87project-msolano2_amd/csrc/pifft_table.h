@@ -13,4 +13,4 @@ struct PassKernel {
 
 }  // namespace pifft
 
-#define PIFFT_NPART 6
+#define PIFFT_NPART 8

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("PIFFT_LIB") or os.path.join(HERE, "libpifft.so")  # P
 CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64
-OUT_NATURAL, OUT_SLICES = 0, 1
+OUT_NATURAL, OUT_SLICES, OUT_BITREV = 0, 1, 2
 KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass"}
 
 

@@ -45,6 +45,13 @@ extern "C" {
 #define PIFFT_OUT_NATURAL 0 /* device output in natural order (needs count == P)   */
 #define PIFFT_OUT_SLICES 1  /* device output slice-major: worker q's N/P bins
                                Z_q[k] = X[bitrev(q) + P k] contiguous, q = first.. */
+#define PIFFT_OUT_BITREV 2  /* the reference's own scratch order (tmp_in after the
+                               cylinder, CPU.c:463-478, before its scatter
+                               CPU.c:496-499): slice-major, each slice in
+                               bit-reversed order, S_q[i] = Z_q[bitrev_{log2 M}(i)]
+                               = X[bitrev_{log2 N}(q M + i)]; with all workers on
+                               one plan this is X in bit-reversed order (no
+                               interleave launch) */
 
 typedef struct pifft_plan pifft_plan;
 
@@ -88,7 +95,7 @@ int pifft_plan_create(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t 
 /* Workers [first, first+count) of a P-worker split on `device` (one GPU of a
  * multi-GPU job; the reference's run_thread for each of those Pi).  count must
  * be a power of two dividing first.  flags: PIFFT_OUT_NATURAL (only when
- * count == workers) or PIFFT_OUT_SLICES. */
+ * count == workers), PIFFT_OUT_SLICES or PIFFT_OUT_BITREV. */
 int pifft_plan_create_slices(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t first,
                              uint32_t count, uint32_t batch, int prec, int device, int flags);
 
@@ -126,7 +133,9 @@ int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int max_launches)
  * to the device (untimed), runs, and if host_out != NULL writes this plan's
  * bins at their natural-order positions of host_out (batch*N values; other
  * positions untouched -- the reference's workers write disjoint `out` entries,
- * CPU.c:496-499).  ms_stage1 / ms_stage2 receive the device time of the tree
+ * CPU.c:496-499).  A PIFFT_OUT_BITREV plan instead writes its workers'
+ * scratch segments at host_out[b N + q M + i] (the reference's tmp_in
+ * layout, q = first..first+count-1).  ms_stage1 / ms_stage2 receive the device time of the tree
  * stage and of the rest (the reference's two timers, CPU.c:414-481). */
 int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double* ms_stage1,
                   double* ms_stage2);

@@ -382,6 +382,21 @@ def test_cli_tsv_and_dump(tmp_path):
     got = np.fromfile(out, dtype=np.complex128)
     x = oracle.generate(4096, np.complex128, seed=7)
     assert_bins_close(got, oracle.fft(x, P=4), "f64", 4096)
+    # -r: the reference's scratch order, on one GPU and split over two plans
+    for g in ("1", "2"):
+        r = _cli(["-n", "4096", "-p", "4", "-f", "64", "-s", "7", "-w", str(out), "-o", "-r", "-g", g])
+        if g == "2" and pifft.gpu_count() < 2:
+            continue
+        assert r.returncode == 0, r.stderr
+        got = np.fromfile(out, dtype=np.complex128)
+        assert_bins_close(got, oracle.fft(x, P=4)[_bitrev_perm(4096)], "f64", 4096)
+
+
+@pytest.mark.parametrize("P", ["1", "2", "8"])
+def test_cli_known_answer_scratch_order(P):
+    r = _cli(["-t", "-p", P, "-r"])
+    assert r.returncode == 0, r.stderr
+    assert "Output is correct. Test passed." in r.stdout
 
 
 # ------------------------------------------------- fused tree + first pass ---
@@ -472,3 +487,71 @@ def test_reference_run_with_pifft_backend(prec):
     assert len(cols) == 5 and cols[:2] == ["1048576", "8"]
     r = subprocess.run([exe, "-n", "1048576"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 1 and "Missing option: -p" in r.stderr
+
+
+# ------------------------------------- bit-reversed (reference scratch) order ---
+def _bitrev_perm(n):
+    bits = n.bit_length() - 1
+    i = np.arange(n, dtype=np.uint64)
+    r = np.zeros(n, dtype=np.uint64)
+    for b in range(bits):
+        r |= ((i >> np.uint64(b)) & np.uint64(1)) << np.uint64(bits - 1 - b)
+    return r.astype(np.int64)
+
+
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("n", [8, 64, 1024, 4096])
+def test_bitrev_output_is_reference_scratch(suf, n):
+    """PIFFT_OUT_BITREV == the reference's tmp_in after the cylinder stage
+    (CPU.c:463-478): its scatter out[bitrev(i)] = tmp_in[i] (CPU.c:496-499)
+    is a pure permutation, so tmp_in = golden X[bitrev_N(i)] exactly."""
+    x, X = load_fft(suf, n)
+    want = X[_bitrev_perm(n)]
+    for P in (1, 2, 8):
+        if P > n:
+            continue
+        got = run(pifft.Plan(n, P, 1, PREC[suf], first=0, count=P, device=0, flags=pifft.OUT_BITREV), x)
+        assert_bins_close(got, want, suf, n)
+
+
+@pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("logn,P,batch", [(16, 1, 3), (20, 8, 1), (22, 4, 2), (24, 1, 1)])
+def test_bitrev_output_vs_oracle(suf, logn, P, batch):
+    """Multi-pass local FFTs (the last Stockham pass stores bit-reversed), all
+    workers and single-worker plans, batched; vs the oracle permuted."""
+    n = 1 << logn
+    m = n // P
+    xs = [oracle.generate(n, DT[suf], seed=0x5EED + b) for b in range(batch)]
+    Xs = [oracle.fft(x, P=P, nthreads=8) for x in xs]
+    perm = _bitrev_perm(n)
+    d_in = dev(np.concatenate(xs))
+    plan = pifft.Plan(n, P, batch, PREC[suf], first=0, count=P, device=0, flags=pifft.OUT_BITREV)
+    d_out = torch.empty(batch * n, dtype=d_in.dtype, device="cuda")
+    plan.execute_device(d_in.data_ptr(), d_out.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().reshape(batch, n)
+    for b in range(batch):
+        assert_bins_close(got[b], Xs[b][perm], suf, n)
+    if P > 1:
+        q = P - 2
+        p1 = pifft.Plan(n, P, batch, PREC[suf], first=q, count=1, device=0, flags=pifft.OUT_BITREV)
+        d1 = torch.empty(batch * m, dtype=d_in.dtype, device="cuda")
+        p1.execute_device(d_in.data_ptr(), d1.data_ptr(), torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        g1 = d1.cpu().numpy().reshape(batch, m)
+        for b in range(batch):
+            assert_bins_close(g1[b], Xs[b][perm][q * m:(q + 1) * m], suf, n)
+
+
+def test_bitrev_host_boundary_segments():
+    """pifft_execute on a PIFFT_OUT_BITREV plan writes the reference's tmp_in
+    segments of its workers at q*M (other positions untouched)."""
+    n, P = 1 << 12, 4
+    x = oracle.generate(n, np.complex128)
+    want = oracle.fft(x, P=P)[_bitrev_perm(n)]
+    out = np.full(n, np.nan + 0j, dtype=np.complex128)
+    plan = pifft.Plan(n, P, 1, pifft.F64, first=2, count=2, device=0, flags=pifft.OUT_BITREV)
+    plan.execute(x, out)
+    m = n // P
+    assert np.all(np.isnan(out[:2 * m]))
+    assert_bins_close(out[2 * m:], want[2 * m:], "f64", n)

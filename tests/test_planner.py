@@ -69,3 +69,21 @@ def test_dry_run_validation():
         pifft.dry_run(8, 16)
     with pytest.raises(pifft.PifftError, match="worker range"):
         pifft.dry_run(64, 8, first=3, count=2)
+
+
+@pytest.mark.parametrize("P", [1, 8])
+def test_bitrev_output_needs_no_interleave(P):
+    """PIFFT_OUT_BITREV (the reference's scratch order): the
+    whole transform on one GPU skips the interleave launch."""
+    nat = pifft.dry_run(1 << 20, P, 1, F64)
+    d = pifft.dry_run(1 << 20, P, 1, F64, flags=pifft.OUT_BITREV)
+    assert "interleave" not in d["launch_kind"]
+    assert d["num_launches"] == nat["num_launches"] - (1 if P > 1 else 0)
+    assert d["out_elems"] == 1 << 20
+
+
+def test_bitrev_output_slices_and_bad_flags():
+    d = pifft.dry_run(1 << 28, 8, 1, F64, first=3, count=1, flags=pifft.OUT_BITREV)
+    assert d["launch_kind"][0] == "tree+pass" and d["out_elems"] == (1 << 28) // 8
+    with pytest.raises(pifft.PifftError):
+        pifft.dry_run(1 << 10, 2, 1, F64, flags=7)

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--variants", default="[{}]")
+    ap.add_argument("--flags", type=int, default=-1, help="plan flags (default: natural / slices)")
     args = ap.parse_args()
     import torch
     import pifft
@@ -55,7 +56,8 @@ def main():
             del os.environ[k]
         os.environ.update({k: str(v) for k, v in var.items()})
         count = args.count or args.workers
-        plan = pifft.Plan(n, args.workers, args.batch, prec, first=args.first, count=count, device=0)
+        plan = pifft.Plan(n, args.workers, args.batch, prec, first=args.first, count=count, device=0,
+                          flags=None if args.flags < 0 else args.flags)
         d = plan.describe()
         if y is None or y.numel() != d["out_elems"]:
             y = torch.empty(d["out_elems"], dtype=cdt, device="cuda")
