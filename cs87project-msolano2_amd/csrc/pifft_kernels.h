@@ -150,9 +150,15 @@ __device__ __forceinline__ void dft(cx<T>* v) {
 // selects non-temporal (nt) loads/stores for it -- a win when a pass streams
 // more than the 256 MiB Infinity Cache holds, a loss when the data would
 // otherwise stay resident there (measured).
+#ifndef PIFFT_NT_LOADS
+#define PIFFT_NT_LOADS 1  // build-time switches for A/B variants (tools/mkvariant.sh)
+#endif
+#ifndef PIFFT_NT_STORES
+#define PIFFT_NT_STORES 1
+#endif
 template <bool NTS, typename T>
 __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
-    if constexpr (NTS) {
+    if constexpr (NTS && PIFFT_NT_LOADS) {
         cx<T> r;
         r.re = __builtin_nontemporal_load(&p->re);
         r.im = __builtin_nontemporal_load(&p->im);
@@ -163,7 +169,7 @@ __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
 }
 template <bool NTS, typename T>
 __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
-    if constexpr (NTS) {
+    if constexpr (NTS && PIFFT_NT_STORES) {
         __builtin_nontemporal_store(v.re, &p->re);
         __builtin_nontemporal_store(v.im, &p->im);
     } else {
@@ -353,12 +359,63 @@ struct Stage {
     static constexpr int NB = R / q;
     static constexpr int ns = 1 << (4 * S);
     static constexpr bool cfast = first ? (MODE != 0) : (last ? (MODE == 2) : false);  // MODE 3 as MODE 1
+#ifndef PIFFT_WAVE_PRIVATE
+#define PIFFT_WAVE_PRIVATE 3  // bit 0: whole-line stages (a), bit 1: beta groups (b)
+#endif
+    // Wave-private exchanges (no workgroup barrier into this stage).
+    // (a) b-fast stage after a b-fast radix-16 stage (one butterfly per
+    //     thread) whose R/16 butterflies per line divide 64: every wave holds
+    //     whole lines, and this stage keeps each wave on the same lines.
+    static constexpr int NBP = R / 16;
+    static constexpr bool whole_lines = (PIFFT_WAVE_PRIVATE & 1) && !first && !cfast && (S >= 2 || MODE == 0) &&
+                                        Sh::Q == 16 && NBP <= 64 && 64 % NBP == 0 && NT % 64 == 0;
+    static constexpr int LPW = whole_lines ? 64 / NBP : 1;  // lines per wave
+    // (b) MODE 2, three stages, middle + (c-fast) last stage: last-stage
+    //     butterflies beta + 16 m (m < 16) read exactly the outputs of the
+    //     middle-stage butterflies beta + 16 k (k < QL).  A wave owns the same
+    //     beta groups on all C lines in both stages (lanes across lines).
+    static constexpr bool grouped = (PIFFT_WAVE_PRIVATE & 2) && MODE == 2 && Sh::NSTG == 3 && S >= 1 && Sh::Q == 16 &&
+                                    64 % C == 0 && (64 / C) % Sh::QL == 0 && NT % 64 == 0;
+    static constexpr int GPW = grouped ? 64 / (C * Sh::QL) : 1;  // beta groups per wave
+    static constexpr bool wave_private = whole_lines || (grouped && last);
     __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
-        const int g = tid + u * NT;
-        if constexpr (cfast) { c = g % C; b = g / C; }
-        else { c = g / NB; b = g % NB; }
+        if constexpr (grouped) {
+            const int w = tid >> 6, lane = tid & 63;
+            c = lane % C;
+            if constexpr (!last) {  // one butterfly per thread
+                const int slot = lane / C;
+                b = (w * GPW + slot / Sh::QL) + 16 * (slot % Sh::QL);
+            } else {
+                const int slot = (u * 64 + lane) / C;
+                b = (w * GPW + slot % GPW) + 16 * (slot / GPW);
+            }
+        } else if constexpr (cfast) {
+            const int g = tid + u * NT;
+            c = g % C; b = g / C;
+        } else if constexpr (whole_lines) {
+            const int i = u * 64 + (tid & 63);
+            c = (tid >> 6) * LPW + i / NB; b = i % NB;
+        } else {
+            const int g = tid + u * NT;
+            c = g / NB; b = g % NB;
+        }
     }
 };
+
+// The LDS hand-off between two stages: a workgroup barrier, or -- when each
+// wave reads back only what it wrote itself -- a fence that keeps the
+// compiler from moving the wave's LDS loads above its stores (a wave's LDS
+// instructions complete in order).
+template <bool WAVE>
+__device__ __forceinline__ void lds_handoff() {
+    if constexpr (WAVE) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __syncthreads();
+    }
+}
 
 template <typename T, int R, int C, int MODE, bool NTS, int LP, int S>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
@@ -507,7 +564,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         using Nx = Stage<R, C, BM, S + 1, VPT>;
 #pragma unroll
         for (int comp = 0; comp < 2; comp++) {
-            __syncthreads();
+            // (the tile's first LDS store has no earlier reader to wait for)
+            if (S > 0 || comp > 0) lds_handoff<Nx::wave_private>();
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 int c, b;
@@ -516,7 +574,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #pragma unroll
                 for (int k = 0; k < q; k++) lds[c * LS + lds_pad(base + k * ns)] = comp ? v[u * q + k].im : v[u * q + k].re;
             }
-            __syncthreads();
+            lds_handoff<Nx::wave_private>();
 #pragma unroll
             for (int u = 0; u < Nx::U; u++) {
                 int c, b;
@@ -547,7 +605,10 @@ __global__ __launch_bounds__((PassCfg<R, C, vpt_of<T>()>::NT),
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     cx<T> v[PassShape<R, vpt_of<T>()>::Q];
-    pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, threadIdx.x,
+    // one tile per workgroup: a persistent tile loop (1, 2 or 4 resident
+    // workgroups per CU walking the tiles) measured 1.4-1.7x slower at 2^28
+    // fp64
+    pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, (int)threadIdx.x,
                                            tile_of_block(blockIdx.x, a.log_xg, gridDim.x));
 }
 

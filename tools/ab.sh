@@ -3,7 +3,7 @@
 #   tools/ab.sh "<tune.py args>" variants/a.so variants/b.so ...
 # runs tools/tune.py once per variant, twice round-robin (box drift shows).
 args="$1"; shift
-for round in 1 2; do
+for round in $(seq 1 "${AB_ROUNDS:-2}"); do
   for lib in "$@"; do
     echo "== $lib (round $round)"
     PIFFT_LIB="$lib" timeout -k 10 120 python tools/tune.py $args 2>&1 | grep -v amdgpu.ids || exit 1

@@ -15,7 +15,7 @@
 typedef double __attribute__((ext_vector_type(2))) d2;
 
 template <int Q>
-__global__ void tile_copy(const d2* __restrict__ in, d2* __restrict__ out, int C, int R, int log_s, int strided_in) {
+__global__ __launch_bounds__(512) void tile_copy(const d2* __restrict__ in, d2* __restrict__ out, int C, int R, int log_s, int strided_in) {
     const int NT = blockDim.x;
     const uint64_t tile = blockIdx.x;
     const uint64_t S = 1ull << log_s;
@@ -76,6 +76,28 @@ int main() {
                 printf("%d\t%d\t%s\t%llu\t%.0f\n", C, R, sin ? "read-strided" : "write-strided",
                        (unsigned long long)(S * 16 / 1024), 2.0 * n * 16 / ms / 1e6);
             }
+    }
+    // occupancy: the same C=8 x R=1024 strided-read tile, with dynamic LDS
+    // reserved so that only 1, 2 or 3 workgroups fit per CU (the pass kernel
+    // holds ~70 KiB LDS and ~126 VGPRs: 2 per CU)
+    (void)hipFuncSetAttribute((const void*)tile_copy<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const int lds_kib[] = {0, 40, 60, 75, 100};
+    for (int li = 0; li < 5; li++) {
+        const int C = 8, R = 1024, log_s = 18;
+        const uint64_t tiles = n / ((uint64_t)C * R);
+        const size_t lds = (size_t)lds_kib[li] * 1024;
+        for (int it = 0; it < 2; it++)
+            hipLaunchKernelGGL(tile_copy<16>, dim3(tiles), dim3(512), lds, 0, a, b, C, R, log_s, 1);
+        (void)hipEventRecord(e0, 0);
+        for (int it = 0; it < 4; it++)
+            hipLaunchKernelGGL(tile_copy<16>, dim3(tiles), dim3(512), lds, 0, a, b, C, R, log_s, 1);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        ms /= 4;
+        printf("occupancy\tC=8 R=1024 read-strided\tlds %d KiB\t%.3f ms\t%.0f GB/s\n", lds_kib[li], ms,
+               2.0 * n * 16 / ms / 1e6);
     }
     return 0;
 }
