@@ -106,6 +106,9 @@ def main() -> None:
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (use with --dist-backend gloo)")
+    ap.add_argument("--as-rank", default="",
+                    help="q/G: run only rank q's plan of a G-GPU job, on this one GPU and without a process "
+                         "group (per-rank profiling, e.g. tools/pmc_traffic.py); never a job-level number")
     args = ap.parse_args()
 
     import torch
@@ -114,6 +117,13 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    emulated = None
+    if args.as_rank:
+        if world > 1:
+            raise SystemExit("--as-rank is a single-process option")
+        emulated = tuple(int(v) for v in args.as_rank.split("/"))
+        if len(emulated) != 2 or not 0 <= emulated[0] < emulated[1]:
+            raise SystemExit("--as-rank wants q/G with 0 <= q < G")
     gpu = 0 if args.same_device else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -133,9 +143,13 @@ def main() -> None:
                 dist.barrier()
 
     n = 1 << args.log_n
-    P = args.workers or world
     import pifft_dist
-    first, count = pifft_dist.worker_range(rank, world, P)
+    if emulated:
+        P = args.workers or emulated[1]
+        first, count = pifft_dist.worker_range(emulated[0], emulated[1], P)
+    else:
+        P = args.workers or world
+        first, count = pifft_dist.worker_range(rank, world, P)
     prec = pifft.F64 if args.prec == 64 else pifft.F32
     cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
     esz = 16 if prec == pifft.F64 else 8
@@ -228,6 +242,7 @@ def main() -> None:
                 "launches": launches,
                 "parallelism": f"pi-split p{P} over {world} GPU(s)",
                 "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),
+                "emulated_rank": args.as_rank or None,
             },
             "roofline": {
                 "bound": "hbm",
@@ -242,7 +257,7 @@ def main() -> None:
             },
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not emulated and not args.no_cpu_baseline:
             threads = args.cpu_threads
             ncpu = os.cpu_count() or 1
             while threads > ncpu:
