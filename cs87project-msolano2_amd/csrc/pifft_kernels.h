@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace pifft {
 
 template <typename T>
@@ -260,6 +262,67 @@ __device__ __forceinline__ cx<T> tree_path(cx<T>* v, const TreeTw& tw, uint64_t 
     return v[0];
 }
 
+// w_NS^e = (cos 2 pi e/NS, -sin 2 pi e/NS), e < NS, evaluated at compile time
+// (Taylor series on the first quadrant, then the quadrant's exact rotation)
+template <int NS>
+struct RootsOf {
+    double re[NS], im[NS];
+    constexpr RootsOf() : re(), im() {
+        constexpr double two_pi = 6.283185307179586476925286766559;
+        for (int e = 0; e < NS; e++) {
+            const int quad = (4 * e) / NS, r = e - quad * (NS / 4);
+            const double x = two_pi * r / NS;  // [0, pi/2)
+            double c = 1, s = x, tc = 1, ts = x;
+            for (int i = 1; i < 16; i++) {
+                tc *= -x * x / ((2 * i - 1) * (2 * i));
+                ts *= -x * x / ((2 * i) * (2 * i + 1));
+                c += tc;
+                s += ts;
+            }
+            const double cq = quad == 0 ? c : quad == 1 ? -s : quad == 2 ? -c : s;
+            const double sq = quad == 0 ? s : quad == 1 ? c : quad == 2 ? -s : -c;
+            re[e] = cq;
+            im[e] = -sq;
+        }
+    }
+};
+
+// tree_path for a thread's k-th first-pass input z_q[zi], zi = zi0 + k M/Q
+// (the fused first pass): its level-t twiddle w_N^{(zi + ml M) 2^t} is
+// bt[t] = w_N^{zi0 2^t} times the compile-time constant w_{QP}^{(k + Q ml) 2^t}
+// (N = P M), so a thread needs log2 P table lookups instead of up to 2P per
+// input.  Not bitwise vs the reference (the standalone k_tree is); tolerance.
+template <typename T, int LP, int Q, int K>
+__device__ __forceinline__ cx<T> tree_path_steps(cx<T>* v, const cx<T>* bt, uint32_t q) {
+    constexpr int NS = Q << LP;
+    constexpr RootsOf<NS> roots{};
+#pragma unroll
+    for (int t = 0; t < LP; t++) {
+        const int H = (1 << LP) >> (t + 1);
+        if ((q >> (LP - 1 - t)) & 1) {
+#pragma unroll
+            for (int ml = 0; ml < H; ml++) {
+                const int e = ((K + Q * ml) << t) & (NS - 1);
+                const cx<T> s{(T)roots.re[e], (T)roots.im[e]};
+                v[ml] = cmul(csub(v[ml], v[ml + H]), cmul(bt[t], s));
+            }
+        } else {
+#pragma unroll
+            for (int ml = 0; ml < H; ml++) v[ml] = cadd(v[ml], v[ml + H]);
+        }
+    }
+    return v[0];
+}
+
+// for (I = B; I < E; I += S) f(integral_constant<I>) -- compile-time indices
+template <int B, int E, int S, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + S, E, S>(f);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Stockham pass
 // ---------------------------------------------------------------------------
@@ -431,8 +494,12 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns, LS = Sh::LS;
-    const uint64_t lb_mask = (1ull << a.log_lb) - 1;
-    const uint64_t ns_mask = (1ull << a.log_ns) - 1;
+    // (run-time even where the mode fixes them -- M/R = 1 for a single pass,
+    // Ns = 1 for a first pass: compile-time values measured 2 % slower there)
+    const uint32_t log_lb = a.log_lb;
+    const uint32_t log_ns = a.log_ns;
+    const uint64_t lb_mask = (1ull << log_lb) - 1;
+    const uint64_t ns_mask = (1ull << log_ns) - 1;
 
     // MODE 2: the inter-pass twiddle factors depend only on (line, b); their
     // two-level table entries are fetched with the data, not after it (a
@@ -463,36 +530,40 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             const bool ok = line < a.nlines;
-            const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
-            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.log_lb);
+            const uint64_t bt = line >> log_lb, j = line & lb_mask;
+            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << log_lb);
             if constexpr (BM == 3) {
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
                 // to P = 8 at 128 VGPRs
                 constexpr int P = 1 << LP;
                 constexpr int G = P >= 8 ? 1 : 8 / P;
-                const uint32_t log_m = a.log_lb + Sh::LOGR;
+                const uint32_t log_m = log_lb + Sh::LOGR;
+                // this thread's base twiddles w_N^{zi0 2^t}, zi0 = its k = 0 input
+                const uint64_t zi0 = j + ((uint64_t)b << log_lb);
+                C2 bt[LP];
 #pragma unroll
-                for (int k0 = 0; k0 < q; k0 += G) {
+                for (int t = 0; t < LP; t++) bt[t] = tree_tw<T>(a.tree, zi0 << t);
+                static_for<0, q, G>([&](auto k0c) {
+                    constexpr int k0 = decltype(k0c)::value;
                     C2 w[G][P];
 #pragma unroll
                     for (int g = 0; g < G; g++) {
-                        const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << a.log_lb);
+                        const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << log_lb);
 #pragma unroll
                         for (int m = 0; m < P; m++)
                             w[g][m] = ok ? ld_stream<NTS>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
                     }
-#pragma unroll
-                    for (int g = 0; g < G; g++) {
-                        const uint64_t zi = j + ((uint64_t)(b + (k0 + g) * NB) << a.log_lb);
-                        v[u * q + k0 + g] = tree_path<T, LP>(w[g], a.tree, zi, log_m, a.worker);
-                    }
+                    static_for<0, G, 1>([&](auto gc) {
+                        constexpr int g = decltype(gc)::value;
+                        v[u * q + k0 + g] = tree_path_steps<T, LP, q, k0 + g>(w[g], bt, a.worker);
+                    });
                     __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
-                }
+                });
             } else {
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ok ? ld_stream<NTS>(src + ((uint64_t)(k * NB) << a.log_lb)) : C2{(T)0, (T)0};
+                    v[u * q + k] = ok ? ld_stream<NTS>(src + ((uint64_t)(k * NB) << log_lb)) : C2{(T)0, (T)0};
             }
         }
     }
@@ -543,19 +614,19 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
-                const uint64_t bt = line >> a.log_lb, j = line & lb_mask;
-                const uint64_t pos = ((j >> a.log_ns) << (a.log_ns + Sh::LOGR)) + (j & ns_mask) + ((uint64_t)b << a.log_ns);
+                const uint64_t bt = line >> log_lb, j = line & lb_mask;
+                const uint64_t pos = ((j >> log_ns) << (log_ns + Sh::LOGR)) + (j & ns_mask) + ((uint64_t)b << log_ns);
                 C2* dst = out + bt * a.out_bstride;
                 if constexpr (BREV) {
-                    const uint32_t sh = 64 - (a.log_lb + Sh::LOGR);  // log2 M bits
+                    const uint32_t sh = 64 - (log_lb + Sh::LOGR);  // log2 M bits
 #pragma unroll
                     for (int k = 0; k < q; k++) {
-                        const uint64_t pk = pos + ((uint64_t)(k * NB) << a.log_ns);
+                        const uint64_t pk = pos + ((uint64_t)(k * NB) << log_ns);
                         dst[sh < 64 ? __builtin_bitreverse64(pk) >> sh : 0] = v[u * q + k];
                     }
                 } else {
 #pragma unroll
-                    for (int k = 0; k < q; k++) st_stream<NTS>(dst + pos + ((uint64_t)(k * NB) << a.log_ns), v[u * q + k]);
+                    for (int k = 0; k < q; k++) st_stream<NTS>(dst + pos + ((uint64_t)(k * NB) << log_ns), v[u * q + k]);
                 }
             }
         }
