@@ -41,8 +41,9 @@ def test_config4_split_fuses_the_tree(P):
     assert d["local_n"] == (1 << 28) // P and d["out_elems"] == (1 << 28) // P
     # the fused pass reads the whole input replica once and writes the worker's N/P
     assert d["launch_bytes"][0] == ((1 << 28) + (1 << 28) // P) * 16
-    # heavy first pass: smallest radix first (widest row segments)
-    assert d["radix"][0] == min(d["radix"])
+    # fused first pass: the larger radix first (R = 512, C = 16 measured 1-3 %
+    # faster than the widest row segments at P = 4, 8)
+    assert d["radix"][0] == max(d["radix"])
 
 
 def test_config5_2e32_one_worker_of_8():
