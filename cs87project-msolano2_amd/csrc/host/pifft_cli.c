@@ -349,7 +349,7 @@ int run(tr_t* t) {
             uint64_t bytes = 0;
             for (uint32_t g = 0; g < G; g++) {
                 pifft_plan_get_info(plans[g], &info);
-                for (int i = 0; i < info.num_launches && i < 64; i++) bytes += info.launch_bytes[i];
+                for (int i = 0; i < info.num_launches && i < PIFFT_MAX_LAUNCH_INFO; i++) bytes += info.launch_bytes[i];
             }
             const double ms = s1 + s2;
             const double flops = 5.0 * (double)t->N * log2((double)t->N) * t->batch;

@@ -114,15 +114,15 @@ const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int l
 // ---------------------------------------------------------------------------
 // plan
 // ---------------------------------------------------------------------------
-enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4 };
-enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, NBUF = 5 };
+enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4, STEP_CHUNK_A = 5, STEP_CHUNK_B = 6 };
+enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, BUF_CH = 5, NBUF = 6 };
 
 struct Step {
     int kind = 0;
     const void* fn = nullptr;
     dim3 grid, block;
     size_t lds = 0;
-    int src = BUF_IN, dst = BUF_OUT;
+    int src = -1, dst = -2;  // -1 / -2: the chain element's input / output buffer
     uint64_t src_off = 0, dst_off = 0;  // elements
     PassArgs pa{};
     TreeArgs ta{};
@@ -149,7 +149,8 @@ struct pifft_plan {
     int prof_steps = 0, prof_used = 0;
     int radix[8] = {0}, lines[8] = {0};
     void* buf[NBUF] = {nullptr};
-    size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0;
+    size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0, bytes_ch = 0;
+    int chunk_pairs = 0;  // chunked last-two-pass pairs (one per chunk)
     void* d_tw = nullptr;
     size_t tw_bytes = 0;
     hipStream_t stream = nullptr;
@@ -366,6 +367,97 @@ void release(pifft_plan* p) {
     delete p;
 }
 
+struct Elem {
+    std::vector<Step> steps;
+};
+
+// The last two passes (a, b) of a plan of >= 3 passes whose data exceed the
+// Infinity Cache, run as chunked pairs (PassArgs: line map, virtual sides):
+// per chunk, pass a streams its inputs from HBM (nt loads) into a scratch
+// buffer of PIFFT_CHUNK_MIB MiB with plain stores, and pass b reads the
+// scratch back -- from the Infinity Cache -- and streams its outputs to HBM
+// (nt stores).  Off by default: measured on MI355X (profiles/r01_tune_chunked
+// .log) the pair runs at the same per-pass rate from the cache as from HBM
+// (C4 at 128 MiB chunks: 4.72 vs 4.81-4.84 ms, within box drift; the 8-way
+// split at 2^28 loses 6-20 %), i.e. the passes are bound by their own
+// load/exchange/store pipeline near 5.2-5.8 TB/s, not by HBM.  A chunk is W consecutive residues d < L = M/(Ra Rb) of
+// one transform, or, when a whole transform fits, a group of transforms.
+// Replaces the chain's last two elements with one.
+int chunk_last_two(pifft_plan* p, const std::vector<PassChoice>& passes, std::vector<Elem>& chain, bool dry) {
+    const int chunk_mib = env_int("PIFFT_CHUNK_MIB", 0);
+    const size_t k = passes.size();
+    if (chunk_mib <= 0 || k < 3 || p->bitrev || chain.size() < 2) return 0;
+    const PassChoice &ca = passes[k - 2], &cb = passes[k - 1];
+    if (ca.mode != 2 || cb.mode != 2 || ca.nts != 1 || cb.nts != 1) return 0;
+    const PassKernel* ka = find_pass(p->prec, ca.R, ca.C, 2, 2);
+    const PassKernel* kb = find_pass(p->prec, cb.R, cb.C, 2, 3);
+    if (!ka || !kb) return 0;
+    const Step sa = chain[chain.size() - 2].steps.at(0), sb = chain[chain.size() - 1].steps.at(0);
+    if (sa.kind != STEP_PASS || sb.kind != STEP_PASS) return 0;
+    const uint64_t M = p->m, ntrans = (uint64_t)p->batch * p->nq;
+    const uint64_t Ra = (uint64_t)ca.R, Rb = (uint64_t)cb.R, L = M / (Ra * Rb);
+    const uint64_t ce = ((uint64_t)chunk_mib << 20) / p->esz;  // chunk elements
+    Elem e;
+    auto add = [&](Step s, const PassKernel* kk, int kind, uint64_t nlines) {
+        s.kind = kind;
+        s.fn = kk->fn;
+        s.pa.nlines = nlines;
+        s.grid = dim3((unsigned)((nlines + kk->C - 1) / kk->C));
+        s.bytes = 2 * nlines * (uint64_t)kk->R * p->esz;
+        e.steps.push_back(s);
+    };
+    if (M <= ce) {
+        // whole transforms: groups of G through the scratch, unchanged addressing
+        const uint64_t G = ce / M;
+        if (ntrans < 2) return 0;  // the whole job fits the Infinity Cache anyway
+        for (uint64_t g0 = 0; g0 < ntrans; g0 += G) {
+            const uint64_t gi = std::min(G, ntrans - g0);
+            Step a = sa, b = sb;
+            a.src_off = g0 * M;
+            a.dst = BUF_CH;
+            a.src = -1;
+            b.src = BUF_CH;
+            b.dst_off = g0 * M;
+            add(a, ka, STEP_CHUNK_A, gi * (M / Ra));
+            add(b, kb, STEP_CHUNK_B, gi * (M / Rb));
+        }
+        p->bytes_ch = (size_t)std::min(G, ntrans) * M * p->esz;
+    } else {
+        uint64_t W = ce / (Ra * Rb);
+        if (W < (uint64_t)std::max(ka->C, kb->C) || W >= L) return 0;
+        const uint32_t log_w = (uint32_t)ilog2u(W), log_l = (uint32_t)ilog2u(L);
+        if (ntrans * (L / W) * 2 > PIFFT_MAX_LAUNCH_INFO - 16) return 0;
+        for (uint64_t bt = 0; bt < ntrans; bt++) {
+            for (uint64_t d0 = 0; d0 < L; d0 += W) {
+                Step a = sa, b = sb;
+                a.src_off = bt * M;
+                a.dst = BUF_CH;
+                a.pa.d0 = b.pa.d0 = d0;
+                a.pa.wmask = b.pa.wmask = W - 1;
+                a.pa.log_sh = b.pa.log_sh = log_l - log_w;
+                // pass a: global reads; stores as a transform of W Ra Rb points (Ns = W)
+                a.pa.wr_virt = 1;
+                a.pa.out_log_ns = log_w;
+                // pass b: reads that transform (line stride W Ra); global stores
+                b.src = BUF_CH;
+                b.dst_off = bt * M;
+                b.pa.rd_virt = 1;
+                b.pa.in_log_es = log_w + (uint32_t)ilog2u(Ra);
+                add(a, ka, STEP_CHUNK_A, W * Rb);
+                add(b, kb, STEP_CHUNK_B, W * Ra);
+            }
+        }
+        p->bytes_ch = (size_t)W * Ra * Rb * p->esz;
+    }
+    for (auto& s : e.steps)
+        if (s.lds > 65536 && !dry) (void)hipFuncSetAttribute(s.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
+    p->chunk_pairs = (int)(e.steps.size() / 2);
+    chain.pop_back();
+    chain.pop_back();
+    chain.push_back(e);
+    return 0;
+}
+
 // dry: plan only (pifft_plan_dry_run) -- no device, no allocation
 int build_plan(pifft_plan* p, bool dry = false) {
     const size_t esz = p->esz;
@@ -434,7 +526,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
     p->fused_tree = fused != nullptr;
 
     // --- chain: [tree] [passes] [interleave] ---
-    struct Elem { std::vector<Step> steps; };
     std::vector<Elem> chain;
     const uint64_t M = p->m;
     if (need_tree) {
@@ -516,6 +607,12 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.tw_shift = (uint32_t)(p->log_m - ilog2u(ns) - logr);
         s.pa.log_xg = (uint32_t)env_int((passes[i].mode & 3) == 0 ? "PIFFT_XCD_GROUP_SINGLE" : "PIFFT_XCD_GROUP",
                                         (passes[i].mode & 3) == 0 ? 0 : 2);
+        s.pa.d0 = 0;  // identity line map, no virtual side (see PassArgs)
+        s.pa.wmask = ~0ull;
+        s.pa.log_sh = 0;
+        s.pa.rd_virt = s.pa.wr_virt = 0;
+        s.pa.in_log_es = s.pa.log_lb;
+        s.pa.out_log_ns = s.pa.log_ns;
         s.block = dim3((unsigned)k->nt);
         const uint64_t wgs = (s.pa.nlines + k->C - 1) / k->C;
         if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
@@ -534,6 +631,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         e.steps.push_back(s);
         chain.push_back(e);
     }
+    if (chunk_last_two(p, passes, chain, dry)) return -1;
     if (p->natural && p->P > 1) {
         Step s;
         s.kind = STEP_INTERLEAVE;
@@ -557,13 +655,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
         const int src = (i == 0) ? BUF_IN : dst[i - 1];
         if (dst[i] == BUF_W || src == BUF_W) need_w = true;
         for (auto& s : chain[i].steps) {
-            if (s.kind == STEP_TREE) {
-                if (s.src == -1) s.src = src;
-                if (s.dst == -2) s.dst = dst[i];
-            } else {
-                s.src = src;
-                s.dst = dst[i];
-            }
+            if (s.src == -1) s.src = src;
+            if (s.dst == -2) s.dst = dst[i];
             p->steps.push_back(s);
         }
     }
@@ -573,6 +666,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     if (p->bytes_w) HIPCHK(hipMalloc(&p->buf[BUF_W], p->bytes_w));
     if (p->bytes_ta) HIPCHK(hipMalloc(&p->buf[BUF_TA], p->bytes_ta));
     if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
+    if (p->bytes_ch) HIPCHK(hipMalloc(&p->buf[BUF_CH], p->bytes_ch));
     HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->ev.resize(p->steps.size() + 1);
     for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
@@ -628,13 +722,15 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
 }
 
 int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hipStream_t st) {
-    void* base[NBUF] = {const_cast<void*>(d_in), d_out, p->buf[BUF_W], p->buf[BUF_TA], p->buf[BUF_TB]};
+    void* base[NBUF] = {const_cast<void*>(d_in), d_out, p->buf[BUF_W], p->buf[BUF_TA], p->buf[BUF_TB], p->buf[BUF_CH]};
     const char* src = (const char*)base[s.src] + s.src_off * p->esz;
     char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
     hipError_t e = hipSuccess;
     switch (s.kind) {
         case STEP_PASS:
-        case STEP_TREE_PASS: {
+        case STEP_TREE_PASS:
+        case STEP_CHUNK_A:
+        case STEP_CHUNK_B: {
             PassArgs a = s.pa;
             a.in = src;
             a.out = dst;
@@ -783,7 +879,8 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     info->local_n = p->m;
     info->in_elems = (uint64_t)p->batch * p->n;
     info->out_elems = out_elems(p);
-    info->workspace_bytes = p->bytes_w + p->bytes_ta + p->bytes_tb + p->tw_bytes;
+    info->workspace_bytes = p->bytes_w + p->bytes_ta + p->bytes_tb + p->bytes_ch + p->tw_bytes;
+    info->chunk_pairs = p->chunk_pairs;
     info->num_launches = (int)p->steps.size();
     info->num_passes = p->npasses;
     info->tree_launches = p->tree_steps;
@@ -791,7 +888,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
         info->radix[i] = p->radix[i];
         info->lines[i] = p->lines[i];
     }
-    for (size_t i = 0; i < p->steps.size() && i < 64; i++) {
+    for (size_t i = 0; i < p->steps.size() && i < PIFFT_MAX_LAUNCH_INFO; i++) {
         info->launch_bytes[i] = p->steps[i].bytes;
         info->launch_kind[i] = p->steps[i].kind;
     }

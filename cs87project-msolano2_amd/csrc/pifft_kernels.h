@@ -158,6 +158,11 @@ __device__ __forceinline__ void dft(cx<T>* v) {
 #ifndef PIFFT_NT_STORES
 #define PIFFT_NT_STORES 1
 #endif
+// NT (k_pass template argument): 0 plain; 1 nt loads and stores; 2 nt loads
+// only; 3 nt stores only (2/3: the two halves of a chunked pass pair whose
+// intermediate stays in the Infinity Cache, see PassArgs)
+constexpr bool nt_loads(int nt) { return nt == 1 || nt == 2; }
+constexpr bool nt_stores(int nt) { return nt == 1 || nt == 3; }
 template <bool NTS, typename T>
 __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
     if constexpr (NTS && PIFFT_NT_LOADS) {
@@ -356,7 +361,29 @@ struct PassArgs {
     // log_xg = g > 0, 2^g consecutive tiles (adjacent line groups) are given
     // to blocks of one XCD.  Needs gridDim.x % (8 << g) == 0 (else identity).
     uint32_t log_xg;
+    // Line map and virtual sides (chunked pass pairs).  The last two passes
+    // (radices Ra, Rb; L = M/(Ra Rb) = Ns of the first) split into L
+    // independent residue classes d: pass-a lines d + s L (s < Rb) feed
+    // exactly pass-b lines d + r L (r < Ra).  A chunk of W consecutive
+    // residues from d0 runs pass a into a scratch buffer small enough to stay
+    // in the Infinity Cache, then pass b out of it: HBM sees one read and one
+    // write of the data for the two passes.  Launch line l (< W * lines per
+    // residue) is global line j = d0 + (l & wmask) + ((l & ~wmask) << log_sh)
+    // (log_sh = log L - log W); the twiddles always use j.  A virtual side
+    // addresses the scratch with l as the line index of a transform of
+    // W Ra Rb points (rd_virt: element stride 2^in_log_es; wr_virt: Stockham
+    // store with Ns = 2^out_log_ns).  Unchunked passes: d0 = 0, wmask = ~0,
+    // log_sh = 0, no virtual side, in_log_es = log_lb, out_log_ns = log_ns.
+    uint64_t d0;
+    uint64_t wmask;
+    uint32_t log_sh;
+    uint32_t rd_virt, wr_virt;
+    uint32_t in_log_es, out_log_ns;
 };
+
+__device__ __forceinline__ uint64_t global_line(const PassArgs& a, uint64_t l) {
+    return a.d0 + (l & a.wmask) + ((l & ~a.wmask) << a.log_sh);
+}
 
 __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, uint32_t nblocks) {
     if (log_xg == 0 || (nblocks & ((8u << log_xg) - 1))) return b;
@@ -441,8 +468,32 @@ struct Stage {
                                     64 % C == 0 && (64 / C) % Sh::QL == 0 && NT % 64 == 0;
     static constexpr int GPW = grouped ? 64 / (C * Sh::QL) : 1;  // beta groups per wave
     static constexpr bool wave_private = whole_lines || (grouped && last);
+    // (c) Register exchange into the last stage: no LDS round trip.  The
+    //     middle radix-16 stage leaves one butterfly per thread (lane l of a
+    //     wave = butterfly l % NBP of line l / NBP, holding elements
+    //     256 (l%NBP / 16) + l%16 + 16 k, k < 16).  A last radix 4 over
+    //     NBP = 64 lanes (R = 1024) is then a 4x4 transpose of register
+    //     quadruples across the wave's four 16-lane rows, a last radix 2 over
+    //     NBP = 32 (R = 512) a 2x2 transpose of register pairs across row
+    //     pairs: cross-lane v_permlane32_swap / v_permlane16_swap (CDNA4)
+    //     instead of an LDS store + load per component.
+    //     PIFFT_PERMLANE bit 0: radix 2 (R = 512), bit 1: radix 4 (R = 1024).
+    //     Measured on MI355X (tools/gpu_round.sh perm): radix 2 in the fused
+    //     tree pass ~0.5 % faster; radix 4 in the C4 first pass 5.5 % SLOWER
+    //     (1.815 vs 1.720 ms: the transposes push the kernel past 128 VGPRs,
+    //     2 spills), so only bit 0 is on by default.
+#ifndef PIFFT_PERMLANE
+#define PIFFT_PERMLANE 1
+#endif
+    static constexpr bool perm = last && !first && !cfast && Sh::Q == 16 && NT % 64 == 0 && Sh::NSTG == 3 &&
+                                 (((PIFFT_PERMLANE & 2) && q == 4 && NBP == 64) ||
+                                  ((PIFFT_PERMLANE & 1) && q == 2 && NBP == 32));
     __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
-        if constexpr (grouped) {
+        if constexpr (perm) {
+            const int lane = tid & 63;
+            c = (tid >> 6) * (64 / NBP) + lane / NBP;
+            b = lane % NBP + NBP * u;
+        } else if constexpr (grouped) {
             const int w = tid >> 6, lane = tid & 63;
             c = lane % C;
             if constexpr (!last) {  // one butterfly per thread
@@ -480,7 +531,34 @@ __device__ __forceinline__ void lds_handoff() {
     }
 }
 
-template <typename T, int R, int C, int MODE, bool NTS, int LP, int S>
+// swap halves across lanes (v_permlane16_swap: odd 16-lane rows of a with even
+// rows of b; v_permlane32_swap: upper 32 lanes of a with lower 32 of b)
+template <int W>
+__device__ __forceinline__ void pl_swap(uint32_t& a, uint32_t& b) {
+    if constexpr (W == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        static_assert(W == 32, "permlane width");
+        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        a = r[0];
+        b = r[1];
+    }
+}
+template <int W, typename T>
+__device__ __forceinline__ void pl_swap(cx<T>& a, cx<T>& b) {
+    constexpr int ND = (int)(sizeof(cx<T>) / 4);
+    uint32_t x[ND], y[ND];
+    __builtin_memcpy(x, &a, sizeof a);
+    __builtin_memcpy(y, &b, sizeof b);
+#pragma unroll
+    for (int d = 0; d < ND; d++) pl_swap<W>(x[d], y[d]);
+    __builtin_memcpy(&a, x, sizeof a);
+    __builtin_memcpy(&b, y, sizeof b);
+}
+
+template <typename T, int R, int C, int MODE, int NTS, int LP, int S>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
     constexpr int VPT = vpt_of<T>();
@@ -513,7 +591,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int u = 0; u < U; u++) {
             int c, b;
             St::map(tid, u, c, b);
-            const uint64_t jm = ((tile * C + c) & lb_mask) & ns_mask;
+            const uint64_t jm = global_line(a, (tile * C + c) & lb_mask) & ns_mask;
             const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
             tw_pre[4 * u + 0] = tlo[e0 & hmask];
             tw_pre[4 * u + 1] = thi[e0 >> a.tw_h];
@@ -530,8 +608,9 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             const bool ok = line < a.nlines;
-            const uint64_t bt = line >> log_lb, j = line & lb_mask;
-            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << log_lb);
+            const uint64_t bt = line >> log_lb, l = line & lb_mask;
+            const uint64_t j = a.rd_virt ? l : global_line(a, l);
+            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.in_log_es);
             if constexpr (BM == 3) {
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
@@ -552,7 +631,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                         const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << log_lb);
 #pragma unroll
                         for (int m = 0; m < P; m++)
-                            w[g][m] = ok ? ld_stream<NTS>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
+                            w[g][m] = ok ? ld_stream<nt_loads(NTS)>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
                     }
                     static_for<0, G, 1>([&](auto gc) {
                         constexpr int g = decltype(gc)::value;
@@ -563,7 +642,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             } else {
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ok ? ld_stream<NTS>(src + ((uint64_t)(k * NB) << log_lb)) : C2{(T)0, (T)0};
+                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << a.in_log_es)) : C2{(T)0, (T)0};
             }
         }
     }
@@ -614,22 +693,42 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
-                const uint64_t bt = line >> log_lb, j = line & lb_mask;
-                const uint64_t pos = ((j >> log_ns) << (log_ns + Sh::LOGR)) + (j & ns_mask) + ((uint64_t)b << log_ns);
+                const uint64_t bt = line >> log_lb, l = line & lb_mask;
+                const uint64_t j = a.wr_virt ? l : global_line(a, l);
+                const uint32_t lns = a.out_log_ns;
+                const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
                 C2* dst = out + bt * a.out_bstride;
                 if constexpr (BREV) {
                     const uint32_t sh = 64 - (log_lb + Sh::LOGR);  // log2 M bits
 #pragma unroll
                     for (int k = 0; k < q; k++) {
-                        const uint64_t pk = pos + ((uint64_t)(k * NB) << log_ns);
+                        const uint64_t pk = pos + ((uint64_t)(k * NB) << lns);
                         dst[sh < 64 ? __builtin_bitreverse64(pk) >> sh : 0] = v[u * q + k];
                     }
                 } else {
 #pragma unroll
-                    for (int k = 0; k < q; k++) st_stream<NTS>(dst + pos + ((uint64_t)(k * NB) << log_ns), v[u * q + k]);
+                    for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + pos + ((uint64_t)(k * NB) << lns), v[u * q + k]);
                 }
             }
         }
+    } else if constexpr (Stage<R, C, BM, S + 1, VPT>::perm) {
+        // ---- exchange with the last stage across lanes (Stage::perm) ----
+        // quadruple g: row m, register 4g+j holds element 256 m + 16 (4g+j) + i;
+        // afterwards it holds element 256 j + 16 (4g+m) + i (input j of
+        // butterfly 64 g + 16 m + i)
+        if constexpr (Stage<R, C, BM, S + 1, VPT>::q == 4) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                pl_swap<32>(v[4 * g + 0], v[4 * g + 2]);
+                pl_swap<32>(v[4 * g + 1], v[4 * g + 3]);
+                pl_swap<16>(v[4 * g + 0], v[4 * g + 1]);
+                pl_swap<16>(v[4 * g + 2], v[4 * g + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int g = 0; g < 8; g++) pl_swap<16>(v[2 * g], v[2 * g + 1]);
+        }
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1>(a, lds, v, tid, tile);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
         using Nx = Stage<R, C, BM, S + 1, VPT>;
@@ -667,8 +766,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 // MODE 3: first pass with the tree stage fused in (one worker, P = 2^LP):
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
-// NTS: non-temporal streaming of the data (see ld_stream)
-template <typename T, int R, int C, int MODE, bool NTS, int LP>
+// NTS: non-temporal streaming of the data (nt_loads / nt_stores)
+template <typename T, int R, int C, int MODE, int NTS, int LP>
 __global__ __launch_bounds__((PassCfg<R, C, vpt_of<T>()>::NT),
                              (MODE == 3 && LP >= 4 && PassCfg<R, C, vpt_of<T>()>::waves_per_eu > 2
                                   ? 2

@@ -13,7 +13,7 @@ using namespace pifft;
 
 #define PK(T, PREC, R, C, MODE, NTS, LP)                                                               \
     PassKernel {                                                                                       \
-        PREC, R, C, MODE, NTS, LP, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS != 0, LP>), \
+        PREC, R, C, MODE, NTS, LP, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS, LP>), \
             PassCfg<R, C, vpt_of<T>()>::NT, PassCfg<R, C, vpt_of<T>()>::lds_elems * (int)sizeof(T)                              \
     }
 

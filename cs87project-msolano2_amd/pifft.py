@@ -20,7 +20,8 @@ CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64
 OUT_NATURAL, OUT_SLICES, OUT_BITREV = 0, 1, 2
-KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass"}
+KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass", 5: "chunk-a", 6: "chunk-b"}
+MAX_LAUNCH_INFO = 256  # PIFFT_MAX_LAUNCH_INFO (include/pifft.h)
 
 
 class PifftError(RuntimeError):
@@ -46,8 +47,9 @@ class PlanInfo(ctypes.Structure):
         ("tree_launches", ctypes.c_int32),
         ("radix", ctypes.c_int32 * 8),
         ("lines", ctypes.c_int32 * 8),
-        ("launch_bytes", ctypes.c_uint64 * 64),
-        ("launch_kind", ctypes.c_int32 * 64),
+        ("chunk_pairs", ctypes.c_int32),
+        ("launch_bytes", ctypes.c_uint64 * MAX_LAUNCH_INFO),
+        ("launch_kind", ctypes.c_int32 * MAX_LAUNCH_INFO),
     ]
 
 
@@ -222,8 +224,9 @@ def describe_info(i: PlanInfo) -> dict:
         "out_elems": i.out_elems, "workspace_bytes": i.workspace_bytes, "num_launches": nl,
         "num_passes": i.num_passes, "tree_launches": i.tree_launches,
         "radix": list(i.radix[: i.num_passes]), "lines": list(i.lines[: i.num_passes]),
-        "launch_bytes": list(i.launch_bytes[: min(nl, 64)]),
-        "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, 64)]],
+        "launch_bytes": list(i.launch_bytes[: min(nl, MAX_LAUNCH_INFO)]),
+        "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, MAX_LAUNCH_INFO)]],
+        "chunk_pairs": i.chunk_pairs,
     }
 
 

@@ -55,6 +55,8 @@ extern "C" {
 
 typedef struct pifft_plan pifft_plan;
 
+#define PIFFT_MAX_LAUNCH_INFO 256 /* launches described by pifft_plan_info */
+
 typedef struct pifft_plan_info {
     uint64_t n;              /* transform length N                                */
     uint32_t workers;        /* P                                                 */
@@ -73,9 +75,12 @@ typedef struct pifft_plan_info {
     int32_t tree_launches;   /* launches of the tree ("funnel") stage              */
     int32_t radix[8];        /* LDS-resident sub-FFT length of each pass           */
     int32_t lines[8];        /* columns per workgroup of each pass                 */
-    uint64_t launch_bytes[64]; /* algorithmic HBM bytes of each launch (read+write,
-                                  twiddle tables excluded)                         */
-    int32_t launch_kind[64]; /* 1 tree, 2 pass, 3 interleave, 4 tree fused into a pass */
+    int32_t chunk_pairs;     /* chunked last-two-pass pairs (2 launches each; 0 = none) */
+    uint64_t launch_bytes[PIFFT_MAX_LAUNCH_INFO]; /* algorithmic bytes of each launch
+                                  (read+write of the data, twiddle tables excluded) */
+    int32_t launch_kind[PIFFT_MAX_LAUNCH_INFO]; /* 1 tree, 2 pass, 3 interleave, 4 tree fused
+                                  into a pass, 5 / 6 first / second half of a chunked
+                                  pass pair (intermediate in the Infinity Cache) */
 } pifft_plan_info;
 
 /* Last error message of the calling thread ("" if none). */

@@ -555,3 +555,63 @@ def test_bitrev_host_boundary_segments():
     m = n // P
     assert np.all(np.isnan(out[:2 * m]))
     assert_bins_close(out[2 * m:], want[2 * m:], "f64", n)
+
+
+# --------------------------------------------------- chunked pass pairs ---
+def _plan_env(monkeypatch, env, *a, **k):
+    for key, v in env.items():
+        monkeypatch.setenv(key, str(v))
+    try:
+        return pifft.Plan(*a, **k)
+    finally:
+        for key in env:
+            monkeypatch.delenv(key)
+
+
+@pytest.mark.parametrize("suf,logn,P,batch,env", [
+    ("f64", 22, 1, 1, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 16}),   # 4 residue chunks
+    ("f64", 21, 1, 4, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 64}),   # groups of 2 whole transforms
+    ("f32", 24, 1, 1, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 16}),   # 8 residue chunks
+    ("f64", 24, 4, 1, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 16}),   # fused tree + chunked pair
+    ("f64", 24, 1, 1, {"PIFFT_CHUNK_MIB": 128}),                 # 2 chunks at the natural NT threshold
+])
+def test_chunked_pass_pair(suf, logn, P, batch, env, monkeypatch):
+    """The last two passes run chunk by chunk through an Infinity-Cache-sized
+    scratch: same arithmetic per element, so the result must equal the
+    unchunked plan bit for bit, and the oracle within tolerance."""
+    n = 1 << logn
+    q = P - 1
+    kw = dict(first=q, count=1, device=0, flags=pifft.OUT_SLICES) if P > 1 else {}
+    chunked = _plan_env(monkeypatch, env, n, P, batch, PREC[suf], **kw)
+    d = chunked.describe()
+    assert d["chunk_pairs"] >= 2 and "chunk-a" in d["launch_kind"] and "chunk-b" in d["launch_kind"]
+    plain = _plan_env(monkeypatch, dict(env, PIFFT_CHUNK_MIB=0), n, P, batch, PREC[suf], **kw)
+    assert plain.describe()["chunk_pairs"] == 0
+    x = np.concatenate([oracle.generate(n, DT[suf], seed=logn + b) for b in range(batch)])
+    got = run(chunked, x)
+    assert np.array_equal(got.view(np.uint8), run(plain, x).view(np.uint8))
+    if logn <= 22:
+        for b in range(batch):
+            want = oracle.fft(x[b * n:(b + 1) * n], P=8, nthreads=8)
+            if P > 1:
+                want = pifft_dist.slice_of_natural(want, P, q)
+            m = n // P
+            assert_bins_close(got[b * m:(b + 1) * m], want, suf, n)
+
+
+def test_chunked_pass_pair_config4_bitwise(monkeypatch):
+    """Config 4 (fp64 2^28, one GPU): the chunked plan equals the unchunked one
+    bit for bit (the property tests above check it against the DFT)."""
+    n = 1 << 28
+    x = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=torch.cuda.current_stream())
+    chunked = _plan_env(monkeypatch, {"PIFFT_CHUNK_MIB": 128}, n, 1, 1, pifft.F64)
+    assert chunked.describe()["chunk_pairs"] > 0
+    a = torch.empty_like(x)
+    chunked.execute_device(x.data_ptr(), a.data_ptr(), torch.cuda.current_stream())
+    del chunked
+    plain = _plan_env(monkeypatch, {"PIFFT_CHUNK_MIB": 0}, n, 1, 1, pifft.F64)
+    b = torch.empty_like(x)
+    plain.execute_device(x.data_ptr(), b.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(torch.view_as_real(a), torch.view_as_real(b))

@@ -31,7 +31,40 @@ def test_config4_2e28_fp64():
     d = pifft.dry_run(1 << 28, 1, 1, F64)
     assert d["radix"] == [1024, 512, 512] and d["lines"] == [8, 16, 16]
     assert d["launch_bytes"] == [2 * (1 << 28) * 16] * 3
-    assert d["workspace_bytes"] >= 4 * GiB
+    assert d["workspace_bytes"] >= 4 * GiB and d["chunk_pairs"] == 0
+
+
+def test_config4_chunked_pairs(monkeypatch):
+    """PIFFT_CHUNK_MIB=128: pass 1 through HBM, passes 2+3 as chunked pairs
+    through a 128 MiB (Infinity-Cache sized) scratch: 32 chunks of 32
+    residues, 2 launches each, same algorithmic bytes."""
+    monkeypatch.setenv("PIFFT_CHUNK_MIB", "128")
+    d = pifft.dry_run(1 << 28, 1, 1, F64)
+    assert d["launch_kind"] == ["pass"] + ["chunk-a", "chunk-b"] * 32 and d["chunk_pairs"] == 32
+    assert d["launch_bytes"][0] == 2 * (1 << 28) * 16
+    assert d["launch_bytes"][1:] == [2 * (128 << 20)] * 64
+    assert sum(d["launch_bytes"]) == 3 * 2 * (1 << 28) * 16
+    assert d["workspace_bytes"] >= 4 * GiB + (128 << 20)
+
+
+def test_chunked_pair_rules(monkeypatch):
+    """Chunking (PIFFT_CHUNK_MIB > 0) applies to the last two passes of
+    >= 3-pass plans whose passes stream more than the Infinity Cache."""
+    monkeypatch.setenv("PIFFT_CHUNK_MIB", "128")
+    d = pifft.dry_run(1 << 24, 1, 1, F64)  # 256 MiB each side
+    assert d["chunk_pairs"] == 2 and d["launch_kind"] == ["pass"] + ["chunk-a", "chunk-b"] * 2
+    assert pifft.dry_run(1 << 20, 1, 1, F64)["chunk_pairs"] == 0      # two passes
+    assert pifft.dry_run(1 << 22, 1, 1, F64)["chunk_pairs"] == 0      # cache-resident
+    assert pifft.dry_run(4096, 1, 4096, F32)["chunk_pairs"] == 0      # single pass
+    # bit-reversed output keeps its MODE 6 last pass
+    assert pifft.dry_run(1 << 28, 1, 1, F64, flags=pifft.OUT_BITREV)["chunk_pairs"] == 0
+    # batched transforms that each fit the scratch: groups of whole transforms
+    monkeypatch.setenv("PIFFT_NT", "1")
+    monkeypatch.setenv("PIFFT_CHUNK_MIB", "64")
+    d = pifft.dry_run(1 << 21, 1, 4, F64)
+    assert d["chunk_pairs"] == 2 and d["launch_bytes"][1:] == [2 * (64 << 20)] * 4
+    monkeypatch.setenv("PIFFT_CHUNK_MIB", "0")
+    assert pifft.dry_run(1 << 28, 1, 1, F64)["chunk_pairs"] == 0
 
 
 @pytest.mark.parametrize("P", [2, 4, 8, 16])
