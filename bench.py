@@ -73,8 +73,9 @@ def cpu_baseline(log_n: int, threads: int) -> dict | None:
                       f"worker 0 tree+cylinder {ms:.1f} ms, join wall {wall:.1f} ms"}
 
 
-def load_traffic(config_key: str, launch_index: int):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary."""
+def load_traffic(config_key: str, launch_indices):
+    """HBM bytes per launch of the dominant kernel (mean over its launches) from
+    the committed PMC summary."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
     for f in reversed(files):
         try:
@@ -83,9 +84,9 @@ def load_traffic(config_key: str, launch_index: int):
             continue
         if d.get("config_key") == config_key:
             per = d.get("per_launch_bytes", {})
-            v = per.get(str(launch_index))
-            if v is not None:
-                return float(v), os.path.relpath(f, ROOT)
+            vals = [per.get(str(i)) for i in launch_indices]
+            if vals and all(v is not None for v in vals):
+                return float(sum(vals)) / len(vals), os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -199,13 +200,21 @@ def main() -> None:
         del gathered, natural
 
     avg = [s / args.steps for s in sums]
-    dom = max(range(nl), key=lambda i: avg[i]) if nl else 0
-    dom_bytes = desc["launch_bytes"][dom] if dom < len(desc["launch_bytes"]) else 0
-    achieved = dom_bytes / (avg[dom] * 1e-3) / 1e9 if avg and avg[dom] > 0 else 0.0
+    # dominant kernel = the kernel function with the largest share of the step
+    # (its launches grouped as rocprofv3 --stats groups them); achieved = its
+    # algorithmic bytes per launch / its mean launch duration
+    by_fn = {}
+    for i in range(nl):
+        by_fn.setdefault(desc["launch_fn"][i], []).append(i)
+    dom_launches = max(by_fn.values(), key=lambda ls: sum(avg[i] for i in ls)) if nl else [0]
+    dom = dom_launches[0]
+    dom_ms = sum(avg[i] for i in dom_launches) / len(dom_launches)
+    dom_bytes = sum(desc["launch_bytes"][i] for i in dom_launches) // len(dom_launches)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     flops = 5.0 * n * args.log_n * args.batch
     value = flops / (ms_per_step * 1e-3) / 1e9
     config_key = f"n2^{args.log_n}_f{args.prec}_b{args.batch}_P{P}_q{count}"
-    traffic, traffic_src = load_traffic(config_key, dom)
+    traffic, traffic_src = load_traffic(config_key, dom_launches)
 
     launches = []
     for i in range(nl):
@@ -246,7 +255,8 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"launch {dom} ({launches[dom]['kind'] if launches else '?'})",
+                "kernel": (f"{launches[dom]['kind'] if launches else '?'} kernel of launches {dom_launches} "
+                           f"(mean launch {dom_ms:.4f} ms, HIP events on the launch stream)"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -888,9 +888,14 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
         info->radix[i] = p->radix[i];
         info->lines[i] = p->lines[i];
     }
+    std::vector<const void*> fns;
     for (size_t i = 0; i < p->steps.size() && i < PIFFT_MAX_LAUNCH_INFO; i++) {
         info->launch_bytes[i] = p->steps[i].bytes;
         info->launch_kind[i] = p->steps[i].kind;
+        size_t f = 0;
+        while (f < fns.size() && fns[f] != p->steps[i].fn) f++;
+        if (f == fns.size()) fns.push_back(p->steps[i].fn);
+        info->launch_fn[i] = (int32_t)f;
     }
     return 0;
 }

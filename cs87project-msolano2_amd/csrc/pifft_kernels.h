@@ -381,8 +381,13 @@ struct PassArgs {
     uint32_t in_log_es, out_log_ns;
 };
 
+// The line map is compiled only into the chunked-pair instances (NTS 2 / 3):
+// unchunked passes keep the plain index path (the run-time map cost ~1 % on
+// the C4 mode-2 passes, tools/ab.sh)
+template <int NTS>
 __device__ __forceinline__ uint64_t global_line(const PassArgs& a, uint64_t l) {
-    return a.d0 + (l & a.wmask) + ((l & ~a.wmask) << a.log_sh);
+    if constexpr (NTS == 2 || NTS == 3) return a.d0 + (l & a.wmask) + ((l & ~a.wmask) << a.log_sh);
+    else return l;
 }
 
 __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, uint32_t nblocks) {
@@ -591,7 +596,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int u = 0; u < U; u++) {
             int c, b;
             St::map(tid, u, c, b);
-            const uint64_t jm = global_line(a, (tile * C + c) & lb_mask) & ns_mask;
+            const uint64_t jm = global_line<NTS>(a, (tile * C + c) & lb_mask) & ns_mask;
             const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
             tw_pre[4 * u + 0] = tlo[e0 & hmask];
             tw_pre[4 * u + 1] = thi[e0 >> a.tw_h];
@@ -609,14 +614,19 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const uint64_t line = tile * C + c;
             const bool ok = line < a.nlines;
             const uint64_t bt = line >> log_lb, l = line & lb_mask;
-            const uint64_t j = a.rd_virt ? l : global_line(a, l);
-            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << a.in_log_es);
+            constexpr bool CHUNK = NTS == 2 || NTS == 3;
+            const uint64_t j = (CHUNK && a.rd_virt) ? l : global_line<NTS>(a, l);
+            const uint32_t les = CHUNK ? a.in_log_es : log_lb;
+            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << les);
             if constexpr (BM == 3) {
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
                 // to P = 8 at 128 VGPRs
                 constexpr int P = 1 << LP;
-                constexpr int G = P >= 8 ? 1 : 8 / P;
+#ifndef PIFFT_TREE_LOADS
+#define PIFFT_TREE_LOADS 8  // leaf loads in flight per thread and round
+#endif
+                constexpr int G = P >= PIFFT_TREE_LOADS ? 1 : PIFFT_TREE_LOADS / P;
                 const uint32_t log_m = log_lb + Sh::LOGR;
                 // this thread's base twiddles w_N^{zi0 2^t}, zi0 = its k = 0 input
                 const uint64_t zi0 = j + ((uint64_t)b << log_lb);
@@ -642,7 +652,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             } else {
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << a.in_log_es)) : C2{(T)0, (T)0};
+                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << les)) : C2{(T)0, (T)0};
             }
         }
     }
@@ -694,8 +704,9 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
                 const uint64_t bt = line >> log_lb, l = line & lb_mask;
-                const uint64_t j = a.wr_virt ? l : global_line(a, l);
-                const uint32_t lns = a.out_log_ns;
+                constexpr bool CHUNK = NTS == 2 || NTS == 3;
+                const uint64_t j = (CHUNK && a.wr_virt) ? l : global_line<NTS>(a, l);
+                const uint32_t lns = CHUNK ? a.out_log_ns : (uint32_t)log_ns;
                 const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
                 C2* dst = out + bt * a.out_bstride;
                 if constexpr (BREV) {

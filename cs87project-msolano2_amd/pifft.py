@@ -50,6 +50,7 @@ class PlanInfo(ctypes.Structure):
         ("chunk_pairs", ctypes.c_int32),
         ("launch_bytes", ctypes.c_uint64 * MAX_LAUNCH_INFO),
         ("launch_kind", ctypes.c_int32 * MAX_LAUNCH_INFO),
+        ("launch_fn", ctypes.c_int32 * MAX_LAUNCH_INFO),
     ]
 
 
@@ -227,6 +228,7 @@ def describe_info(i: PlanInfo) -> dict:
         "launch_bytes": list(i.launch_bytes[: min(nl, MAX_LAUNCH_INFO)]),
         "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, MAX_LAUNCH_INFO)]],
         "chunk_pairs": i.chunk_pairs,
+        "launch_fn": list(i.launch_fn[: min(nl, MAX_LAUNCH_INFO)]),
     }
 
 

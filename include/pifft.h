@@ -81,6 +81,9 @@ typedef struct pifft_plan_info {
     int32_t launch_kind[PIFFT_MAX_LAUNCH_INFO]; /* 1 tree, 2 pass, 3 interleave, 4 tree fused
                                   into a pass, 5 / 6 first / second half of a chunked
                                   pass pair (intermediate in the Infinity Cache) */
+    int32_t launch_fn[PIFFT_MAX_LAUNCH_INFO]; /* kernel of each launch: launches with the same id
+                                  run the same kernel function (ids 0, 1, ... in order
+                                  of first use) -- what rocprof aggregates per kernel */
 } pifft_plan_info;
 
 /* Last error message of the calling thread ("" if none). */

@@ -13,6 +13,7 @@ tag="${1:-r01}"
 export TMPDIR=/tmp
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || exit 1
 timeout -k 10 300 python -u bench.py > "$out/bench.log" 2>&1 || exit 1
 grep '^{' "$out/bench.log" > "$out/${tag}_bench.json" || exit 1
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$out/stats_c4" -o c4 -- \
