@@ -310,6 +310,29 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         out.push_back({R, C, 0, nts});
         return 0;
     }
+    // tuning: explicit log2 radices, e.g. PIFFT_RADIX_LOGS=10,10,8 (must sum to log2 M)
+    if (const char* rl = getenv("PIFFT_RADIX_LOGS")) {
+        std::vector<int> logs;
+        for (const char* c = rl; *c;) {
+            char* end = nullptr;
+            const long v = strtol(c, &end, 10);
+            if (end == c) break;
+            logs.push_back((int)v);
+            c = *end ? end + 1 : end;
+        }
+        int sum = 0;
+        for (int l : logs) sum += l;
+        if (sum == logm && logs.size() > 1) {
+            for (size_t p = 0; p < logs.size(); p++) {
+                const int R = 1 << logs[p], mode = p == 0 ? 1 : 2;
+                const int C = pick_lines(prec, R, M >> logs[p], ntrans * (M >> logs[p]),
+                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
+                if (!find_pass(prec, R, C, mode, nts)) return fail("no pass kernel R=%d C=%d", R, C);
+                out.push_back({R, C, mode, nts});
+            }
+            return 0;
+        }
+    }
     const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32", 10);
     const int kmin = (logm + rmax_log - 1) / rmax_log;
     const int kmax = env_int("PIFFT_PASSES", 0) > 0 ? env_int("PIFFT_PASSES", 0) : kmin + 1;
@@ -350,6 +373,10 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         }
     }
     if (out.empty()) return fail("no pass decomposition for M=2^%d", logm);
+    // tuning: lines per workgroup of the last pass (its write side's segment width)
+    const int last_c = env_int("PIFFT_LAST_C", 0);
+    if (last_c > 0 && out.size() > 1 && find_pass(prec, out.back().R, last_c, out.back().mode, out.back().nts))
+        out.back().C = last_c;
     return 0;
 }
 
@@ -584,8 +611,12 @@ int build_plan(pifft_plan* p, bool dry = false) {
     p->npasses = (int)passes.size();
     for (size_t i = 0; i < passes.size(); i++) {
         const bool fuse_here = (i == 0 && fused);
+        const bool last_pass = i + 1 == passes.size() && passes.size() > 1;
+        // tuning: the last pass's streaming form (0 plain, 1 nt both, 2 nt loads, 3 nt stores)
+        const int last_nt = last_pass && passes[i].mode == 2 ? env_int("PIFFT_LAST_NT", -1) : -1;
         const PassKernel* k = fuse_here ? fused
-                                        : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode, passes[i].nts);
+                                        : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode,
+                                                    last_nt >= 0 ? last_nt : passes[i].nts);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
@@ -607,6 +638,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.tw_shift = (uint32_t)(p->log_m - ilog2u(ns) - logr);
         s.pa.log_xg = (uint32_t)env_int((passes[i].mode & 3) == 0 ? "PIFFT_XCD_GROUP_SINGLE" : "PIFFT_XCD_GROUP",
                                         (passes[i].mode & 3) == 0 ? 0 : 2);
+        if (last_pass) s.pa.log_xg = (uint32_t)env_int("PIFFT_LAST_XCD_GROUP", (int)s.pa.log_xg);
         s.pa.d0 = 0;  // identity line map, no virtual side (see PassArgs)
         s.pa.wmask = ~0ull;
         s.pa.log_sh = 0;
