@@ -41,6 +41,26 @@ __global__ void tile_k(const f4* __restrict__ in, f4* __restrict__ out, uint64_t
     for (int u = 0; u < U; u++) st<U, NT>(out + base + (uint64_t)u * blockDim.x, v[u]);
 }
 
+// one tile per workgroup, at most W loads in flight per lane (sliding window):
+// does a 128-KiB tile copy gain from fewer bytes in flight chip-wide?
+#define PC_STR2(x) #x
+#define PC_STR(x) PC_STR2(x)
+template <int U, int W>
+__global__ void tile_win_k(const f4* __restrict__ in, f4* __restrict__ out, uint64_t n) {
+    const uint64_t base = (uint64_t)blockIdx.x * blockDim.x * U + threadIdx.x;
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        v[u] = __builtin_nontemporal_load(in + base + (uint64_t)u * blockDim.x);
+        if constexpr (W == 1) { if (u < U - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+        if constexpr (W == 2) { if (u >= 1 && u < U - 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); }
+        if constexpr (W == 4) { if (u >= 3 && u < U - 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); }
+        if constexpr (W == 8) { if (u >= 7 && u < U - 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(v[u], out + base + (uint64_t)u * blockDim.x);
+}
+
 // persistent grid-stride
 template <int U, bool NT>
 __global__ void gs_k(const f4* __restrict__ in, f4* __restrict__ out, uint64_t n) {
@@ -92,5 +112,13 @@ int main() {
     TILE(4, 0, 1, 256) TILE(4, 1, 1, 256) TILE(16, 1, 1, 256) TILE(4, 0, 2, 256) TILE(4, 1, 2, 256) TILE(16, 1, 2, 256)
     GS(4, 0, 256, 1024) GS(4, 1, 256, 1024) GS(4, 1, 256, 2048) GS(4, 1, 256, 4096) GS(8, 1, 256, 2048)
     GS(4, 1, 512, 2048) GS(16, 1, 256, 1024) GS(4, 1, 1024, 1024)
+#define WIN(U, W, BS)                                                                                         \
+    {                                                                                                         \
+        const unsigned grid = (unsigned)(n / ((uint64_t)BS * U));                                             \
+        float ms = timeit([&] { hipLaunchKernelGGL((tile_win_k<U, W>), dim3(grid), dim3(BS), 0, 0, A, B, n); }); \
+        printf("win\tU=%d\tW=%d\tbs=%d\t%.3f ms\t%.0f GB/s\n", U, W, BS, ms, 2.0 * S / ms / 1e6);               \
+    }
+    WIN(16, 16, 512) WIN(16, 8, 512) WIN(16, 4, 512) WIN(16, 2, 512) WIN(16, 1, 512) WIN(16, 16, 512)
+    TILE(1, 1, 0, 256)
     return 0;
 }
