@@ -12,6 +12,10 @@ value = 5 N log2 N / t for the one transform ("strong" scaling: the total work
 is fixed).  Inputs are generated on the device (splitmix64, the oracle's
 generator) and resident in HBM before the timed region.
 
+--shard batch (config 3, e.g. --log-n 12 --prec 32 --batch 4096): the batch of
+independent transforms is split by transform instead, rank r running B/G whole
+transforms (P = --workers, default 1) -- again no data-path collective.
+
 Adds to the JSON line:
   roofline     : the dominant kernel's algorithmic bytes / its mean duration
                  (HIP events on the launch stream, inside the timed region),
@@ -100,6 +104,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--workers", type=int, default=0, help="P (default: number of ranks)")
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--shard", choices=("workers", "batch"), default="workers",
+                    help="split one transform's workers over the ranks (the reference's pi split), or a "
+                         "batch of independent transforms by transform (config 3)")
     ap.add_argument("--allgather", action="store_true", help="also time the optional RCCL all-gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-log-n", type=int, default=26)
@@ -145,25 +152,29 @@ def main() -> None:
 
     n = 1 << args.log_n
     import pifft_dist
-    if emulated:
-        P = args.workers or emulated[1]
-        first, count = pifft_dist.worker_range(emulated[0], emulated[1], P)
+    q_rank, g_world = emulated if emulated else (rank, world)
+    b_first, b_count = 0, args.batch  # transforms of the batch on this rank
+    if args.shard == "batch":
+        P = args.workers or 1
+        first, count = 0, P
+        b_first, b_count = pifft_dist.batch_range(q_rank, g_world, args.batch)
     else:
-        P = args.workers or world
-        first, count = pifft_dist.worker_range(rank, world, P)
+        P = args.workers or g_world
+        first, count = pifft_dist.worker_range(q_rank, g_world, P)
     prec = pifft.F64 if args.prec == 64 else pifft.F32
     cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
     esz = 16 if prec == pifft.F64 else 8
 
     if count == P:
-        plan = pifft.Plan(n, P, args.batch, prec, first=0, count=P, device=gpu, flags=pifft.OUT_NATURAL)
+        plan = pifft.Plan(n, P, b_count, prec, first=0, count=P, device=gpu, flags=pifft.OUT_NATURAL)
     else:
-        plan = pifft.Plan(n, P, args.batch, prec, first=first, count=count, device=gpu,
+        plan = pifft.Plan(n, P, b_count, prec, first=first, count=count, device=gpu,
                           flags=pifft.OUT_SLICES)
     desc = plan.describe()
     stream = torch.cuda.current_stream(dev)
-    x = torch.empty(n * args.batch, dtype=cdt, device=dev)
-    pifft.generate_device(x.data_ptr(), n * args.batch, n, prec, seed=args.seed, stream=stream)
+    # this rank's transforms of the global batch: elements [b_first n, (b_first + b_count) n)
+    x = torch.empty(n * b_count, dtype=cdt, device=dev)
+    pifft.generate_device(x.data_ptr(), n * b_count, n, prec, seed=args.seed, first=b_first * n, stream=stream)
     y = torch.empty(desc["out_elems"], dtype=cdt, device=dev)
     for _ in range(args.warmup):
         plan.execute_device(x.data_ptr(), y.data_ptr(), stream)
@@ -188,7 +199,16 @@ def main() -> None:
     ms_per_step = elapsed * 1e3 / args.steps
 
     allgather_ms = None
-    if args.allgather and dist is not None and count < P:
+    if args.allgather and dist is not None and args.shard == "batch":
+        # whole transforms per rank: the gathered batch is already in order
+        torch.cuda.synchronize(dev)
+        barrier()
+        ta = time.perf_counter()
+        gathered = pifft_dist.allgather_slices(y)
+        torch.cuda.synchronize(dev)
+        allgather_ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
+        del gathered
+    elif args.allgather and dist is not None and count < P:
         torch.cuda.synchronize(dev)
         barrier()
         ta = time.perf_counter()
@@ -211,9 +231,9 @@ def main() -> None:
     dom_ms = sum(avg[i] for i in dom_launches) / len(dom_launches)
     dom_bytes = sum(desc["launch_bytes"][i] for i in dom_launches) // len(dom_launches)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    flops = 5.0 * n * args.log_n * args.batch
+    flops = 5.0 * n * args.log_n * args.batch  # the whole job's batch (every rank's share)
     value = flops / (ms_per_step * 1e-3) / 1e9
-    config_key = f"n2^{args.log_n}_f{args.prec}_b{args.batch}_P{P}_q{count}"
+    config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
     traffic, traffic_src = load_traffic(config_key, dom_launches)
 
     launches = []
@@ -241,15 +261,21 @@ def main() -> None:
             "config": {
                 "workload": (f"config 4: one fp64 complex N=2^{args.log_n} pi-FFT" if args.log_n == 28 and
                              args.prec == 64 and args.batch == 1 else
+                             f"config 3: batched fp32 {args.batch} x N=4096" if args.log_n == 12 and
+                             args.prec == 32 and args.batch == 4096 else
                              f"pi-FFT N=2^{args.log_n} f{args.prec} batch {args.batch}")
-                            + f", P={P} workers, {count} per GPU (no data-path collective)",
+                            + (f", P={P} workers, {b_count} whole transforms per GPU (batch-sharded, no "
+                               f"data-path collective)" if args.shard == "batch" else
+                               f", P={P} workers, {count} per GPU (no data-path collective)"),
                 "n": n, "workers": P, "workers_per_gpu": count, "batch": args.batch,
+                "batch_per_gpu": b_count, "shard": args.shard,
                 "local_n": desc["local_n"], "passes": desc["num_passes"], "radix": desc["radix"],
                 "lines_per_workgroup": desc["lines"],
                 "hbm_bytes_per_step_algorithmic": total_bytes,
                 "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                 "launches": launches,
-                "parallelism": f"pi-split p{P} over {world} GPU(s)",
+                "parallelism": (f"batch-split {args.batch}/{world} per GPU, p{P}" if args.shard == "batch" else
+                                f"pi-split p{P} over {world} GPU(s)"),
                 "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),
                 "emulated_rank": args.as_rank or None,
             },

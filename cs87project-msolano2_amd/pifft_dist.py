@@ -6,6 +6,8 @@ worker range lives on each GPU/rank:
 
   * worker_range(rank, world, P): rank r computes workers [r P/W, (r+1) P/W)
     (the reference's Pi, CPU.c:336) -- no collective on the data path;
+  * batch_range(rank, world, B): for a batch of independent transforms
+    (config 3) rank r runs transforms [r B/W, (r+1) B/W) whole instead;
   * the only optional exchange is the final all-gather of the slices
     (torch.distributed all_gather over RCCL/xGMI, or gloo on CPU) followed by
     the stride-P interleave (interleave_slices / pifft_interleave_device);
@@ -20,6 +22,17 @@ def worker_range(rank: int, world: int, workers: int) -> tuple[int, int]:
     if world < 1 or workers % world:
         raise ValueError(f"{workers} workers cannot be split over {world} ranks")
     per = workers // world
+    return rank * per, per
+
+
+def batch_range(rank: int, world: int, batch: int) -> tuple[int, int]:
+    """Batched transforms (config 3) shard by transform: rank r runs transforms
+    [r B/W, (r+1) B/W) whole, with its own P workers -- independent objects,
+    no exchange.  The reference has no batch; a batch is its
+    run() applied to each vector (CPU.c:312-380)."""
+    if world < 1 or batch < 1 or batch % world:
+        raise ValueError(f"a batch of {batch} transforms cannot be split over {world} ranks")
+    per = batch // world
     return rank * per, per
 
 

@@ -83,3 +83,55 @@ def test_interleave_matches_reference_ownership():
     X = oracle.fft(x)
     sl = np.stack([pifft_dist.slice_of_natural(X, P, q) for q in range(P)])
     assert pifft_dist.interleave_slices(sl).tobytes() == X.tobytes()
+
+
+def _batch_rank_main(rank, world, port, n, batch, q_out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (os.path.join(root, "oracle"), os.path.join(root, "cs87project-msolano2_amd")):
+        sys.path.insert(0, p)
+    import pifft_dist
+    import pifft_oracle as oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first, count = pifft_dist.batch_range(rank, world, batch)
+        # this rank's transforms of the global batch, exactly as bench.py --shard batch generates them
+        x = oracle.generate(n, np.complex64, count=count * n, first=first * n).reshape(count, n)
+        mine = np.stack([oracle.fft(x[b]) for b in range(count)])
+        local = torch.from_numpy(mine.reshape(-1).view(np.float32).copy())
+        gathered = pifft_dist.allgather_slices(local).numpy().view(np.complex64).reshape(batch, n)
+        if rank == 0:
+            xa = oracle.generate(n, np.complex64, count=batch * n).reshape(batch, n)
+            want = np.stack([oracle.fft(xa[b]) for b in range(batch)])
+            q_out.put(gathered.tobytes() == want.tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,batch", [(4096, 8), (256, 6)])
+def test_two_rank_batch_shard_gather_equals_batch(n, batch):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_rank_main, args=(r, world, port, n, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(), "gathered batch shards differ from the per-transform oracle"
+
+
+def test_batch_range():
+    import pifft_dist
+    assert [pifft_dist.batch_range(r, 8, 4096) for r in (0, 7)] == [(0, 512), (3584, 512)]
+    assert pifft_dist.batch_range(0, 1, 5) == (0, 5)
+    with pytest.raises(ValueError):
+        pifft_dist.batch_range(0, 3, 4096)
+    with pytest.raises(ValueError):
+        pifft_dist.batch_range(0, 2, 0)

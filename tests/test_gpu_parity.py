@@ -191,6 +191,20 @@ def test_config3_batched_fp32_4096x4096():
         assert_bins_close(got[i], oracle.fft(xs[i]), "f32", n)
     # whole batch against a float64 numpy FFT (same tolerance)
     assert rel_l2(got, np.fft.fft(xs.astype(np.complex128), axis=1)) <= tol("f32", n)
+    # config 3 on 8 GPUs (bench.py --shard batch): rank r generates and runs
+    # transforms [512 r, 512 (r+1)) of the same batch; its results are those
+    # rows of the 1-GPU batch, bit for bit (same single-pass kernel)
+    for r in (0, 5, 7):
+        first, count = pifft_dist.batch_range(r, 8, b)
+        d_x = torch.empty(count * n, dtype=torch.complex64, device="cuda")
+        pifft.generate_device(d_x.data_ptr(), count * n, n, pifft.F32, first=first * n,
+                              stream=torch.cuda.current_stream())
+        d_y = torch.empty_like(d_x)
+        pifft.Plan(n, 1, count, pifft.F32).execute_device(d_x.data_ptr(), d_y.data_ptr(),
+                                                          torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert d_x.cpu().numpy().tobytes() == x[first * n:(first + count) * n].tobytes(), f"rank {r} input"
+        assert d_y.cpu().numpy().reshape(count, n).tobytes() == got[first:first + count].tobytes(), f"rank {r}"
 
 
 # ------------------------------------------------------------- sweeps/edges ---
