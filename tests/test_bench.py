@@ -1,0 +1,56 @@
+"""bench.py's output contract (the driver parses its one JSON line): keys,
+types, the BASELINE.json metric, the roofline and cpu_baseline objects, and
+the batch-shard mode.  Small sizes; the timing itself is not judged here."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def _common(d, steps, warmup):
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert d["metric"] == json.load(f)["metric"]
+    assert d["unit"] == "GFLOP/s" and d["higher_is_better"] is True
+    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == warmup
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["scaling"] in ("strong", "weak") and d["vs_baseline"] is None
+    n = d["config"]["n"]
+    # value = 5 N log2 N (x batch) / t
+    flops = 5.0 * n * (n.bit_length() - 1) * d["config"]["batch"]
+    assert abs(d["value"] - flops / (d["ms_per_step"] * 1e-3) / 1e9) <= 1e-3 * d["value"] + 0.01
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert 0 < rf["achieved"] and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert rf["algorithmic_bytes"] > 0
+    assert len(d["config"]["launches"]) >= 1
+
+
+def test_bench_default_contract_small():
+    d = _bench("--log-n", "20", "--steps", "3", "--warmup", "1", "--cpu-log-n", "16", "--cpu-threads", "2")
+    _common(d, 3, 1)
+    assert d["dtype"] == "f64" and d["config"]["workers"] == 1 and d["config"]["shard"] == "workers"
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] in ("reference", "port") and cb["sample"]
+
+
+def test_bench_batch_shard_rank_share():
+    d = _bench("--log-n", "12", "--prec", "32", "--batch", "64", "--shard", "batch", "--as-rank", "1/4",
+               "--steps", "3", "--warmup", "1")
+    _common(d, 3, 1)
+    assert d["dtype"] == "f32" and d["config"]["batch_per_gpu"] == 16 and d["config"]["shard"] == "batch"
+    assert d["cpu_baseline"] is None  # emulated rank: never a job-level CPU comparison
