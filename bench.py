@@ -54,19 +54,34 @@ def cpu_baseline(log_n: int, threads: int) -> dict | None:
     n = 1 << log_n
     flops = 5.0 * n * log_n
     exe = oracle.reference_binary(64)
-    if exe:
+    host = {"cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
+
+    def run_ref(path):
         t0 = time.perf_counter()
-        r = subprocess.run([exe, "-n", str(n), "-p", str(threads), "-o"], capture_output=True, text=True,
+        r = subprocess.run([path, "-n", str(n), "-p", str(threads), "-o"], capture_output=True, text=True,
                            timeout=900)
         wall = time.perf_counter() - t0
-        if r.returncode == 0:
-            cols = r.stdout.strip().splitlines()[-1].split("\t")
-            ms = float(cols[2])
-            return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
-                    "kind": "reference",
-                    "sample": f"reference fourier-parallel-pi-cpu-pthreads built -O2 -Dfloat=double, "
-                              f"fp64 N=2^{log_n}, p={threads} pthreads; worker 0's tree+cylinder time "
-                              f"{ms:.1f} ms (the reference's own timer); process wall {wall:.1f} s"}
+        if r.returncode != 0:
+            return None, wall
+        return float(r.stdout.strip().splitlines()[-1].split("\t")[2]), wall
+
+    if exe:
+        ms, wall = run_ref(exe)
+        if ms is not None:
+            out = {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
+                   "kind": "reference",
+                   "sample": f"reference fourier-parallel-pi-cpu-pthreads built -O2 -Dfloat=double, "
+                             f"fp64 N=2^{log_n}, p={threads} pthreads; worker 0's tree+cylinder time "
+                             f"{ms:.1f} ms (the reference's own timer); process wall {wall:.1f} s", **host}
+            # the same at the reference Makefile's own flags (-g, no -O; cpu/Makefile:21)
+            o0 = exe + "-O0"
+            if os.path.exists(o0):
+                ms0, wall0 = run_ref(o0)
+                if ms0 is not None:
+                    out["value_O0"] = round(flops / (ms0 * 1e6), 4)
+                    out["sample_O0"] = (f"same sample, reference built with its Makefile's flags (-g, -O0): "
+                                        f"worker 0 {ms0:.1f} ms, process wall {wall0:.1f} s")
+            return out
     # fallback: the C restatement (bitwise-equal arithmetic)
     import numpy as np
     x = oracle.generate(n, np.complex128)
@@ -74,7 +89,18 @@ def cpu_baseline(log_n: int, threads: int) -> dict | None:
     ms = t1 + t2
     return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads, "kind": "port",
             "sample": f"oracle/pifft_oracle.c (restated reference) fp64 N=2^{log_n}, {threads} threads; "
-                      f"worker 0 tree+cylinder {ms:.1f} ms, join wall {wall:.1f} ms"}
+                      f"worker 0 tree+cylinder {ms:.1f} ms, join wall {wall:.1f} ms", **host}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_traffic(config_key: str, launch_indices):
