@@ -348,8 +348,19 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         for (int order = 0; order < 2; order++) {  // 0: larger radices first, 1: smaller first
             if (force_order >= 0 && order != force_order) continue;
             // a fused tree+first pass runs best with the larger radix (R = 512,
-            // C = 16) first: measured 1-3 % over the model's pick at P = 4, 8
-            if (force_order < 0 && heavy_lp > 0 && order == 1) continue;
+            // C = 16) first: measured 1-3 % over the model's pick at P = 4, 8.
+            // Not when that radix leaves the P-fold leaf reads narrower than
+            // 256-B segments (R = 1024, C = 8 at fp64): then the model picks
+            // between both orders (config 5, 2^29 per worker: 512-1024-1024
+            // 19.7 ms vs 256-128-128-128 21.3 ms, profiles/r01_tune_c5.log).
+            // fp64 only: the fp32 tile gives R = 1024 128-B segments too, but
+            // the other order there loses the fused kernel (no instance)
+            if (force_order < 0 && heavy_lp > 0 && order == 1) {
+                const int R0 = 1 << (base + (extra > 0 ? 1 : 0));
+                const int C0 = pick_lines(prec, R0, M >> ilog2u((uint64_t)R0), ntrans * (M >> ilog2u((uint64_t)R0)),
+                                          prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", 1);
+                if (prec != 64 || (size_t)C0 * esz >= 256) continue;  // fp32: measured cases only
+            }
             std::vector<PassChoice> cand;
             double cost = 0.0;
             bool ok = true;

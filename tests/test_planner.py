@@ -83,6 +83,11 @@ def test_config5_2e32_one_worker_of_8():
     d = pifft.dry_run(1 << 32, 8, 1, F64, first=5, count=1)
     assert d["local_n"] == 1 << 29 and d["launch_kind"][0] == "tree+pass"
     assert d["launch_bytes"][0] == ((1 << 32) + (1 << 29)) * 16
+    # the fused pass keeps 256-B leaf segments (R = 512) and the plan stays at 3 passes: measured
+    # 19.7 ms vs 21.3 ms for 256-128-128-128 (profiles/r01_tune_c5.log)
+    assert d["radix"] == [512, 1024, 1024]
+    # where the larger radix already gives 256-B leaf segments it still goes first (P = 8 at 2^28)
+    assert pifft.dry_run(1 << 28, 8, 1, F64, first=7, count=1)["radix"] == [512, 256, 256]
 
 
 def test_fp32_large_prefers_wide_segments():
