@@ -278,7 +278,7 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(ms_per_step, 6),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
