@@ -415,7 +415,7 @@ def test_cli_known_answer_scratch_order(P):
 
 # ------------------------------------------------- fused tree + first pass ---
 @pytest.mark.parametrize("suf", list(DT))
-@pytest.mark.parametrize("logn,P", [(16, 2), (18, 4), (19, 8), (20, 16), (23, 8), (24, 2), (25, 4), (26, 8)])
+@pytest.mark.parametrize("logn,P", [(16, 2), (18, 4), (19, 8), (20, 16), (22, 2), (23, 8), (24, 2), (24, 8), (25, 4), (26, 8)])
 def test_fused_tree_first_pass(suf, logn, P, monkeypatch):
     """Single-worker plans with a multi-pass local FFT evaluate the tree inside
     the first pass (MODE 3); results must match the oracle and the unfused plan."""
