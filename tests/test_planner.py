@@ -126,3 +126,16 @@ def test_bitrev_output_slices_and_bad_flags():
     assert d["launch_kind"][0] == "tree+pass" and d["out_elems"] == (1 << 28) // 8
     with pytest.raises(pifft.PifftError):
         pifft.dry_run(1 << 10, 2, 1, F64, flags=7)
+
+
+@pytest.mark.parametrize("prec", [F64, F32])
+def test_every_multipass_worker_plan_fuses_its_tree(prec):
+    """One worker of P (one GPU of a P-GPU job) with a multi-pass local FFT
+    evaluates its tree inside the first pass: a fused kernel instance exists
+    for whatever radix and lines the planner picks (fp32 plans once fell back
+    to a separate tree launch for want of one)."""
+    for logn in range(16, 33):
+        for P in (2, 4, 8, 16):
+            d = pifft.dry_run(1 << logn, P, 1, prec, first=P - 1, count=1)
+            if d["num_passes"] > 1:
+                assert d["launch_kind"][0] == "tree+pass", (logn, P, d["radix"], d["lines"])
