@@ -2,6 +2,7 @@
 # tools/ab.sh -- A/B per-launch timing of library variants on one box:
 #   tools/ab.sh "<tune.py args>" variants/a.so variants/b.so ...
 # runs tools/tune.py once per variant, twice round-robin (box drift shows).
+set -o pipefail
 args="$1"; shift
 for round in $(seq 1 "${AB_ROUNDS:-2}"); do
   for lib in "$@"; do
