@@ -1,0 +1,11 @@
+#!/bin/bash
+# tools/gpu_lds_pmc.sh -- LDS counters of the pass kernels (one --pmc pass per
+# plan, SQ block only): C4 and rank 0's plan of the 8-GPU job.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/lds
+C="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES"
+timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d gpurun_out/lds/c4 -o pmc -- \
+    python -u bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/lds/c4.out 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d gpurun_out/lds/p8 -o pmc -- \
+    python -u bench.py --no-cpu-baseline --as-rank 0/8 --steps 2 --warmup 1 > gpurun_out/lds/p8.out 2>&1 || exit 1
