@@ -4,17 +4,26 @@
   "GFLOP/s (5N log2N / t) + % HBM roofline, fp64 complex N=2^28 @1/2/4/8 GPU"
 
 One step = one complete pi-FFT of ONE fp64 complex N=2^28 transform (config 4
-at --gpus 1).  With --gpus G (one process per GPU, torchrun) the same transform
-is split over P=G workers the reference's way: rank q computes worker q's
-N/P output bins (its tree over the whole, replicated input + an N/P-point FFT),
-with no data-path collective; the time is the slowest rank's (max over ranks),
-value = 5 N log2 N / t for the one transform ("strong" scaling: the total work
-is fixed).  Inputs are generated on the device (splitmix64, the oracle's
+at --gpus 1).  With --gpus G the same transform is split over P=G workers the
+reference's way, one process per GPU: rank q computes worker q's N/P output
+bins (its tree over the whole, replicated input + an N/P-point FFT), with no
+data-path collective; the time is the slowest rank's (max over ranks), value =
+5 N log2 N / t for the one transform ("strong" scaling: the total work is
+fixed).  Inputs are generated on the device (splitmix64, the oracle's
 generator) and resident in HBM before the timed region.
+
+--gpus G without a torchrun environment: this process launches G ranks
+(python -m torch.distributed.run, 127.0.0.1) and exits with their status; it
+never touches a GPU itself.  Under torchrun, WORLD_SIZE must equal --gpus.
 
 --shard batch (config 3, e.g. --log-n 12 --prec 32 --batch 4096): the batch of
 independent transforms is split by transform instead, rank r running B/G whole
 transforms (P = --workers, default 1) -- again no data-path collective.
+
+At G > 1 the optional final exchange (RCCL all-gather over xGMI + the
+stride-P interleave into natural order) runs once after the timed region and
+is reported as config.allgather_ms (never part of value; --no-allgather skips
+it).  Every rank's own time and dominant-kernel roofline go to config.per_rank.
 
 Adds to the JSON line:
   roofline     : the dominant kernel's algorithmic bytes / its mean duration
@@ -22,16 +31,22 @@ Adds to the JSON line:
                  vs 8 TB/s; traffic = PMC-measured HBM bytes per launch from the
                  committed rocprofv3 summary (profiles/), else null
   cpu_baseline : the reference CPU path (oracle/_ref, compiled from the
-                 reference source) on a bounded sample, rank 0 at --gpus 1 only
+                 reference source) at the SAME N, rank 0 at --gpus 1 only, with
+                 the largest power-of-two worker count whose (2 + 2P) S bytes
+                 of scratch (CPU.c:396-407) fit the host's memory
+  secondary    : (--gpus 1, default on) configs 1, 2 (whole and one GPU's
+                 slice) and 3 timed in the same run, each with its own
+                 dominant-kernel roofline and a reference CPU baseline at the
+                 same N
 """
 from __future__ import annotations
 
 import argparse
 import glob
 import json
-import math
 import os
-import re
+import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -41,55 +56,12 @@ sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CPU_MEM_CAP = 160 << 30  # never plan a CPU sample above this (the GPU box caps a command near 270 GiB)
 
 
 def _baseline_metric():
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         return json.load(f)["metric"]
-
-
-def cpu_baseline(log_n: int, threads: int) -> dict | None:
-    """Reference CPU path (oracle/_ref, -Dfloat=double) on N=2^log_n with P=threads."""
-    import pifft_oracle as oracle
-    n = 1 << log_n
-    flops = 5.0 * n * log_n
-    exe = oracle.reference_binary(64)
-    host = {"cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
-
-    def run_ref(path):
-        t0 = time.perf_counter()
-        r = subprocess.run([path, "-n", str(n), "-p", str(threads), "-o"], capture_output=True, text=True,
-                           timeout=900)
-        wall = time.perf_counter() - t0
-        if r.returncode != 0:
-            return None, wall
-        return float(r.stdout.strip().splitlines()[-1].split("\t")[2]), wall
-
-    if exe:
-        ms, wall = run_ref(exe)
-        if ms is not None:
-            out = {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
-                   "kind": "reference",
-                   "sample": f"reference fourier-parallel-pi-cpu-pthreads built -O2 -Dfloat=double, "
-                             f"fp64 N=2^{log_n}, p={threads} pthreads; worker 0's tree+cylinder time "
-                             f"{ms:.1f} ms (the reference's own timer); process wall {wall:.1f} s", **host}
-            # the same at the reference Makefile's own flags (-g, no -O; cpu/Makefile:21)
-            o0 = exe + "-O0"
-            if os.path.exists(o0):
-                ms0, wall0 = run_ref(o0)
-                if ms0 is not None:
-                    out["value_O0"] = round(flops / (ms0 * 1e6), 4)
-                    out["sample_O0"] = (f"same sample, reference built with its Makefile's flags (-g, -O0): "
-                                        f"worker 0 {ms0:.1f} ms, process wall {wall0:.1f} s")
-            return out
-    # fallback: the C restatement (bitwise-equal arithmetic)
-    import numpy as np
-    x = oracle.generate(n, np.complex128)
-    _, (t1, t2, wall) = oracle.fft(x, P=threads, nthreads=threads, timing=True)
-    ms = t1 + t2
-    return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/pifft_oracle.c (restated reference) fp64 N=2^{log_n}, {threads} threads; "
-                      f"worker 0 tree+cylinder {ms:.1f} ms, join wall {wall:.1f} ms", **host}
 
 
 def _cpu_model() -> str:
@@ -103,10 +75,93 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _mem_available() -> int:
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 8 << 30
+
+
+def _host() -> dict:
+    return {"cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "mem_available_GiB": round(_mem_available() / 2**30, 1)}
+
+
+def _run_ref(path: str, n: int, p: int, timeout: int = 900):
+    """One run of the reference CLI; (worker 0's tree+cylinder ms by its own timer, wall s)."""
+    t0 = time.perf_counter()
+    r = subprocess.run([path, "-n", str(n), "-p", str(p), "-o"], capture_output=True, text=True, timeout=timeout)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"reference exited {r.returncode}: {r.stderr.strip()[-300:]}")
+    return float(r.stdout.strip().splitlines()[-1].split("\t")[2]), wall
+
+
+def ref_workers(log_n: int, esz: int, threads: int) -> int:
+    """The largest power of two P <= threads whose reference footprint fits:
+    in + out (2 S) plus 2 S of scratch per worker (CPU.c:225-239, 396-407)."""
+    s = (1 << log_n) * esz
+    budget = min(int(_mem_available() * 0.7), CPU_MEM_CAP)
+    p = 1
+    while p * 2 <= threads and (2 + 2 * p * 2) * s <= budget:
+        p *= 2
+    if (2 + 2 * p) * s > budget:
+        raise RuntimeError(f"N=2^{log_n} needs {(2 + 2 * p) * s / 2**30:.0f} GiB of host memory, "
+                           f"{budget / 2**30:.0f} GiB available")
+    return p
+
+
+def cpu_baseline(log_n: int, prec: int, threads: int, workers: int | None = None, repeat: int = 1,
+                 batch: int = 1, slice_of: int = 0) -> dict:
+    """The reference CPU path at N = 2^log_n: oracle/_ref (CPU.c built -O2,
+    -Dfloat=double for fp64) with P = `workers` pthreads (default: as many as
+    the threads and host memory allow).  Its own timer (worker 0's tree +
+    cylinder, CPU.c:414-491) gives the time.  repeat > 1 takes the median of
+    that many runs; batch > 1 scales one transform's time to the batch (the
+    reference has no batch: a batch is a loop of run()).  slice_of = P: the
+    time is ONE worker's share of a P-worker split (worker 0's own time),
+    reported as the rate of the whole transform at that time."""
+    import pifft_oracle as oracle
+    n = 1 << log_n
+    esz = 16 if prec == 64 else 8
+    flops = 5.0 * n * log_n * batch
+    p = workers or ref_workers(log_n, esz, threads)
+    exe = oracle.reference_binary(prec)
+    if exe is None:  # fallback: the C restatement (bitwise-equal arithmetic)
+        import numpy as np
+        x = oracle.generate(n, np.complex128 if prec == 64 else np.complex64)
+        _, (t1, t2, wall) = oracle.fft(x, P=p, nthreads=p, timing=True)
+        ms = (t1 + t2) * batch
+        return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": p, "kind": "port",
+                "sample": f"oracle/pifft_oracle.c (restated reference) f{prec} N=2^{log_n}, P={p}; worker 0 "
+                          f"tree+cylinder {ms:.1f} ms, join wall {wall:.1f} ms", **_host()}
+    runs = [_run_ref(exe, n, p) for _ in range(repeat)]
+    ms1 = statistics.median(r[0] for r in runs)
+    ms = ms1 * batch
+    what = (f"reference fourier-parallel-pi-cpu-pthreads built -O2{' -Dfloat=double' if prec == 64 else ''} "
+            f"(oracle/_ref, from the reference source), f{prec} N=2^{log_n}, p={p} pthreads")
+    if repeat > 1:
+        what += f"; median of {repeat} runs of worker 0's tree+cylinder time {ms1:.3f} ms"
+    else:
+        what += f"; worker 0's tree+cylinder time {ms1:.1f} ms (the reference's own timer)"
+    if batch > 1:
+        what += f" x {batch} transforms (the reference has no batch) = {ms:.1f} ms"
+    if slice_of:
+        what += f"; one worker's share of the {slice_of}-way split, rated as the whole transform"
+    what += f"; process wall {sum(r[1] for r in runs):.1f} s"
+    footprint = (2 + 2 * p) * n * esz
+    return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": p, "kind": "reference",
+            "ms": round(ms, 3), "sample": what, "host_bytes": footprint, **_host()}
+
+
 def load_traffic(config_key: str, launch_indices):
     """HBM bytes per launch of the dominant kernel (mean over its launches) from
-    the committed PMC summary."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
+    the committed PMC summary (the newest profiles/*traffic*.json of this plan)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), key=os.path.getmtime)
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -120,9 +175,187 @@ def load_traffic(config_key: str, launch_indices):
     return None, None
 
 
-def main() -> None:
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(gpus: int) -> int:
+    """--gpus G outside torchrun: one rank process per GPU (this parent never
+    initialises a GPU; it only waits for its children)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class Job:
+    """One pi-FFT plan on this rank's GPU with its input resident in HBM."""
+
+    def __init__(self, pifft, torch, gpu, *, n, P, prec, first, count, batch_local, b_first, seed):
+        self.pifft, self.torch, self.n, self.P = pifft, torch, n, P
+        self.prec, self.count, self.batch_local = prec, count, batch_local
+        self.dev = torch.device("cuda", gpu)
+        flags = pifft.OUT_NATURAL if count == P else pifft.OUT_SLICES
+        self.plan = pifft.Plan(n, P, batch_local, prec, first=first, count=count, device=gpu, flags=flags)
+        self.desc = self.plan.describe()
+        self.stream = torch.cuda.current_stream(self.dev)
+        cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
+        # this rank's transforms of the global batch: elements [b_first n, (b_first + b_local) n)
+        self.x = torch.empty(n * batch_local, dtype=cdt, device=self.dev)
+        pifft.generate_device(self.x.data_ptr(), n * batch_local, n, prec, seed=seed, first=b_first * n,
+                              stream=self.stream)
+        self.y = torch.empty(self.desc["out_elems"], dtype=cdt, device=self.dev)
+
+    def step(self):
+        self.plan.execute_device(self.x.data_ptr(), self.y.data_ptr(), self.stream)
+
+    def run(self, steps, warmup, barrier=lambda: None):
+        """W untimed steps, then exactly K steps between barrier + synchronize
+        on both sides; per-launch HIP events recorded on the launch stream
+        inside the timed region (no host syncs).  Returns this rank's seconds."""
+        torch = self.torch
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize(self.dev)
+        self.plan.profile_start(steps)
+        barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        torch.cuda.synchronize(self.dev)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        recorded, sums = self.plan.profile_read()
+        assert recorded == steps, recorded
+        self.avg = [s / steps for s in sums]
+        return elapsed
+
+    def roofline(self) -> dict:
+        """The dominant kernel (the kernel function with the largest share of
+        the step; its launches grouped as rocprofv3 --stats groups them):
+        algorithmic bytes per launch / its mean launch duration."""
+        d, avg = self.desc, self.avg
+        nl = d["num_launches"]
+        by_fn = {}
+        for i in range(nl):
+            by_fn.setdefault(d["launch_fn"][i], []).append(i)
+        dom_launches = max(by_fn.values(), key=lambda ls: sum(avg[i] for i in ls))
+        dom_ms = sum(avg[i] for i in dom_launches) / len(dom_launches)
+        dom_bytes = sum(d["launch_bytes"][i] for i in dom_launches) // len(dom_launches)
+        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        return {"bound": "hbm",
+                "kernel": (f"{d['launch_kind'][dom_launches[0]]} kernel of launches {dom_launches} "
+                           f"(mean launch {dom_ms:.4f} ms, HIP events on the launch stream)"),
+                "launches": dom_launches, "mean_ms": round(dom_ms, 5),
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": dom_bytes}
+
+    def launches(self) -> list:
+        d, out = self.desc, []
+        for i in range(d["num_launches"]):
+            b = d["launch_bytes"][i]
+            out.append({"kind": d["launch_kind"][i], "bytes": b, "ms": round(self.avg[i], 4),
+                        "GB/s": round(b / (self.avg[i] * 1e-3) / 1e9, 1) if self.avg[i] > 0 else None})
+        return out
+
+    def free(self):
+        self.plan.close()
+        self.x = self.y = None
+        self.torch.cuda.empty_cache()
+
+
+def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_cpu) -> dict:
+    """Configs 1-3 of BASELINE.json on this one GPU, each a separate timed loop
+    (same contract as the headline step) with its own roofline and a reference
+    CPU baseline at the same N."""
+    F64, F32 = pifft.F64, pifft.F32
+    cases = [
+        ("C1", "config 1: fp64 N=2^20, 1 worker", dict(log_n=20, prec=F64, P=1, first=0, count=1, batch=1),
+         dict(log_n=20, prec=64, workers=1, repeat=3)),
+        ("C2", "config 2: fp64 N=2^20, 8 workers on one GPU (natural order)",
+         dict(log_n=20, prec=F64, P=8, first=0, count=8, batch=1), dict(log_n=20, prec=64, workers=8, repeat=5)),
+        ("C2_slice", "config 2, one GPU's slice: worker 0 of the 8-way split (rated as the whole transform)",
+         dict(log_n=20, prec=F64, P=8, first=0, count=1, batch=1),
+         dict(log_n=20, prec=64, workers=8, repeat=5, slice_of=8)),
+        ("C3", "config 3: batched fp32 4096 x N=4096", dict(log_n=12, prec=F32, P=1, first=0, count=1, batch=4096),
+         dict(log_n=12, prec=32, workers=1, repeat=31, batch=4096)),
+    ]
+    out = {}
+    for key, what, g, c in cases:
+        rec = {"workload": what}
+        try:
+            n = 1 << g["log_n"]
+            job = Job(pifft, torch, gpu, n=n, P=g["P"], prec=g["prec"], first=g["first"], count=g["count"],
+                      batch_local=g["batch"], b_first=0, seed=seed)
+            # small steps: more of them, so the timed loop is not launch-jitter
+            k = max(steps, 50)
+            elapsed = job.run(k, max(warmup, 5))
+            ms = elapsed * 1e3 / k
+            flops = 5.0 * n * g["log_n"] * g["batch"]
+            rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
+                        "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],
+                        "workers_in_plan": g["count"], "batch": g["batch"], "passes": job.desc["num_passes"],
+                        "radix": job.desc["radix"], "launches": job.launches(), "roofline": job.roofline()})
+            job.free()
+        except Exception as e:  # reported, never silently replaced
+            rec["error"] = repr(e)
+        if with_cpu:
+            try:
+                rec["cpu_baseline"] = cpu_baseline(threads=cpu_threads, **c)
+            except Exception as e:
+                rec["cpu_baseline"] = {"value": None, "error": repr(e)}
+        out[key] = rec
+    return out
+
+
+def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev) -> dict:
+    """Config 5 on a multi-GPU job: fp64 N=2^32 split over `world` GPUs (one
+    worker per GPU, 64 GiB input replica each), then the RCCL all-gather and
+    interleave into natural order (timed separately)."""
+    import pifft_dist
+    log_n = 32
+    n = 1 << log_n
+    rec = {"workload": f"config 5: fp64 N=2^32 over {world} GPUs, one worker each (no data-path collective), "
+                       f"then the RCCL all-gather + interleave"}
+    job = Job(pifft, torch, gpu, n=n, P=world, prec=pifft.F64, first=rank, count=1, batch_local=1, b_first=0,
+              seed=seed)
+    elapsed = pifft_dist.max_over_ranks(job.run(steps, warmup, barrier), red_dev)
+    ms = elapsed * 1e3 / steps
+    rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
+                "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(),
+                "roofline_rank0": job.roofline() if rank == 0 else None})
+    job.x = None  # the 64 GiB replica is not needed by the exchange
+    torch.cuda.empty_cache()
+    rec["allgather_ms"] = round(allgather(pifft, torch, dist, job, barrier, red_dev), 3)
+    job.free()
+    return rec
+
+
+def allgather(pifft, torch, dist, job, barrier, red_dev) -> float:
+    """The optional final exchange: RCCL all-gather of every rank's slices,
+    then the stride-P interleave into natural order on every GPU (ms, max over
+    ranks)."""
+    import pifft_dist
+    torch.cuda.synchronize(job.dev)
+    barrier()
+    ta = time.perf_counter()
+    gathered = pifft_dist.allgather_slices(job.y)
+    natural = torch.empty(job.n * job.batch_local, dtype=job.y.dtype, device=job.dev)
+    pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), job.n, job.P, job.batch_local, job.prec,
+                            job.stream)
+    torch.cuda.synchronize(job.dev)
+    ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
+    del gathered, natural
+    return ms
+
+
+def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs (= ranks, one process per GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=28)
@@ -133,9 +366,13 @@ def main() -> None:
     ap.add_argument("--shard", choices=("workers", "batch"), default="workers",
                     help="split one transform's workers over the ranks (the reference's pi split), or a "
                          "batch of independent transforms by transform (config 3)")
-    ap.add_argument("--allgather", action="store_true", help="also time the optional RCCL all-gather")
+    ap.add_argument("--allgather", dest="allgather", action="store_true", default=True,
+                    help="at G > 1, time the optional RCCL all-gather + interleave after the timed region (default)")
+    ap.add_argument("--no-allgather", dest="allgather", action="store_false")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip configs 1-3 (at 1 GPU) / config 5 (at 8 GPUs) beside the headline step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-log-n", type=int, default=26)
+    ap.add_argument("--cpu-log-n", type=int, default=0, help="CPU baseline size (default: the headline N)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo")
     ap.add_argument("--same-device", action="store_true",
@@ -145,12 +382,21 @@ def main() -> None:
                          "group (per-rank profiling, e.g. tools/pmc_traffic.py); never a job-level number")
     args = ap.parse_args()
 
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        if args.as_rank:
+            raise SystemExit("--as-rank emulates one rank on one GPU: use it without --gpus")
+        return spawn_ranks(args.gpus)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} does not match the {world} rank(s) launched (WORLD_SIZE)")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
     import torch
     import pifft
+    import pifft_dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     emulated = None
     if args.as_rank:
         if world > 1:
@@ -159,6 +405,9 @@ def main() -> None:
         if len(emulated) != 2 or not 0 <= emulated[0] < emulated[1]:
             raise SystemExit("--as-rank wants q/G with 0 <= q < G")
     gpu = 0 if args.same_device else local
+    if not args.same_device and world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit(f"{world} ranks but only {torch.cuda.device_count()} GPU(s) visible "
+                         f"(rehearse with --same-device --dist-backend gloo)")
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
@@ -176,8 +425,8 @@ def main() -> None:
             else:
                 dist.barrier()
 
+    red_dev = dev if args.dist_backend == "nccl" else None  # gloo reduces on the CPU
     n = 1 << args.log_n
-    import pifft_dist
     q_rank, g_world = emulated if emulated else (rank, world)
     b_first, b_count = 0, args.batch  # transforms of the batch on this rank
     if args.shard == "batch":
@@ -188,89 +437,49 @@ def main() -> None:
         P = args.workers or g_world
         first, count = pifft_dist.worker_range(q_rank, g_world, P)
     prec = pifft.F64 if args.prec == 64 else pifft.F32
-    cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
-    esz = 16 if prec == pifft.F64 else 8
 
-    if count == P:
-        plan = pifft.Plan(n, P, b_count, prec, first=0, count=P, device=gpu, flags=pifft.OUT_NATURAL)
-    else:
-        plan = pifft.Plan(n, P, b_count, prec, first=first, count=count, device=gpu,
-                          flags=pifft.OUT_SLICES)
-    desc = plan.describe()
-    stream = torch.cuda.current_stream(dev)
-    # this rank's transforms of the global batch: elements [b_first n, (b_first + b_count) n)
-    x = torch.empty(n * b_count, dtype=cdt, device=dev)
-    pifft.generate_device(x.data_ptr(), n * b_count, n, prec, seed=args.seed, first=b_first * n, stream=stream)
-    y = torch.empty(desc["out_elems"], dtype=cdt, device=dev)
-    for _ in range(args.warmup):
-        plan.execute_device(x.data_ptr(), y.data_ptr(), stream)
-    torch.cuda.synchronize(dev)
-
-    nl = desc["num_launches"]
-    # per-launch HIP events on the launch stream, recorded inside the timed
-    # region without host syncs (pifft_profile_start/read)
-    plan.profile_start(args.steps)
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        plan.execute_device(x.data_ptr(), y.data_ptr(), stream)
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    recorded, sums = plan.profile_read()
-    assert recorded == args.steps, recorded
-    red_dev = dev if args.dist_backend == "nccl" else None  # gloo reduces on the CPU
-    elapsed = pifft_dist.max_over_ranks(elapsed, red_dev)
+    job = Job(pifft, torch, gpu, n=n, P=P, prec=prec, first=first, count=count, batch_local=b_count,
+              b_first=b_first, seed=args.seed)
+    local_s = job.run(args.steps, args.warmup, barrier)
+    elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms_per_step = elapsed * 1e3 / args.steps
+    rf = job.roofline()
+    desc = job.desc
+    launches = job.launches()
+    config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
+    traffic, traffic_src = load_traffic(config_key, rf["launches"])
+
+    per_rank = None
+    if dist is not None:
+        mine = {"rank": rank, "gpu": gpu, "workers": [first, first + count], "batch": [b_first, b_first + b_count],
+                "ms_per_step": round(local_s * 1e3 / args.steps, 6), "dominant_ms": rf["mean_ms"],
+                "achieved": rf["achieved"], "frac": rf["frac"]}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     allgather_ms = None
-    if args.allgather and dist is not None and args.shard == "batch":
-        # whole transforms per rank: the gathered batch is already in order
-        torch.cuda.synchronize(dev)
-        barrier()
-        ta = time.perf_counter()
-        gathered = pifft_dist.allgather_slices(y)
-        torch.cuda.synchronize(dev)
-        allgather_ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
-        del gathered
-    elif args.allgather and dist is not None and count < P:
-        torch.cuda.synchronize(dev)
-        barrier()
-        ta = time.perf_counter()
-        gathered = pifft_dist.allgather_slices(y)
-        natural = torch.empty(n * args.batch, dtype=cdt, device=dev)
-        pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), n, P, args.batch, prec, stream)
-        torch.cuda.synchronize(dev)
-        allgather_ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
-        del gathered, natural
+    if args.allgather and dist is not None and (args.shard == "batch" or count < P):
+        allgather_ms = allgather(pifft, torch, dist, job, barrier, red_dev)
+    job.free()
 
-    avg = [s / args.steps for s in sums]
-    # dominant kernel = the kernel function with the largest share of the step
-    # (its launches grouped as rocprofv3 --stats groups them); achieved = its
-    # algorithmic bytes per launch / its mean launch duration
-    by_fn = {}
-    for i in range(nl):
-        by_fn.setdefault(desc["launch_fn"][i], []).append(i)
-    dom_launches = max(by_fn.values(), key=lambda ls: sum(avg[i] for i in ls)) if nl else [0]
-    dom = dom_launches[0]
-    dom_ms = sum(avg[i] for i in dom_launches) / len(dom_launches)
-    dom_bytes = sum(desc["launch_bytes"][i] for i in dom_launches) // len(dom_launches)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    secondary = None
+    if not args.no_secondary and not emulated:
+        if world == 1 and args.log_n == 28 and args.prec == 64 and args.batch == 1:
+            secondary = secondary_configs(pifft, torch, gpu, args.steps, args.warmup, args.seed, args.cpu_threads,
+                                          not args.no_cpu_baseline)
+        elif world == 8 and args.shard == "workers" and not args.same_device:
+            try:
+                secondary = {"C5": config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
+                                           min(args.warmup, 2), args.seed, barrier, red_dev)}
+            except Exception as e:  # reported, never silently replaced
+                secondary = {"C5": {"error": repr(e)}}
+
+    total_bytes = sum(desc["launch_bytes"][: desc["num_launches"]])
     flops = 5.0 * n * args.log_n * args.batch  # the whole job's batch (every rank's share)
     value = flops / (ms_per_step * 1e-3) / 1e9
-    config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
-    traffic, traffic_src = load_traffic(config_key, dom_launches)
-
-    launches = []
-    for i in range(nl):
-        kind = desc["launch_kind"][i] if i < len(desc["launch_kind"]) else "?"
-        b = desc["launch_bytes"][i] if i < len(desc["launch_bytes"]) else 0
-        launches.append({"kind": kind, "bytes": b, "ms": round(avg[i], 4),
-                         "GB/s": round(b / (avg[i] * 1e-3) / 1e9, 1) if avg[i] > 0 else None})
-    total_bytes = sum(desc["launch_bytes"][:nl])
-
     if rank == 0:
+        rf_line = {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac")}
+        rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"]})
         line = {
             "metric": _baseline_metric(),
             "value": round(value, 2),
@@ -280,7 +489,7 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 6),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong",  # the job's total work (one transform, or the global batch) is fixed
             "vs_baseline": None,
             "dtype": "f64" if prec == pifft.F64 else "f32",
             "data": "synthetic: splitmix64 U[-1,1]/sqrt(N) complex input generated in HBM (the oracle's generator)",
@@ -303,20 +512,11 @@ def main() -> None:
                 "parallelism": (f"batch-split {args.batch}/{world} per GPU, p{P}" if args.shard == "batch" else
                                 f"pi-split p{P} over {world} GPU(s)"),
                 "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),
+                "per_rank": per_rank,
                 "emulated_rank": args.as_rank or None,
+                "secondary": secondary,
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": (f"{launches[dom]['kind'] if launches else '?'} kernel of launches {dom_launches} "
-                           f"(mean launch {dom_ms:.4f} ms, HIP events on the launch stream)"),
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "algorithmic_bytes": dom_bytes,
-            },
+            "roofline": rf_line,
             "cpu_baseline": None,
         }
         if world == 1 and not emulated and not args.no_cpu_baseline:
@@ -325,13 +525,16 @@ def main() -> None:
             while threads > ncpu:
                 threads //= 2
             try:
-                line["cpu_baseline"] = cpu_baseline(args.cpu_log_n, max(1, threads))
+                cl = args.cpu_log_n or args.log_n
+                line["cpu_baseline"] = cpu_baseline(cl, args.prec, max(1, threads), batch=args.batch,
+                                                    repeat=1 if cl > 16 else 15)
             except Exception as e:  # reported, never silently replaced
                 line["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -28,6 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -157,7 +158,12 @@ struct pifft_plan {
     std::vector<hipEvent_t> ev;
     void* d_hin = nullptr;   // pifft_execute's staging copies
     void* d_hout = nullptr;
+    void* d_gather = nullptr;  // pifft_allgather: every worker's slices on this plan's device
     std::vector<char> host_tmp;
+    std::vector<int> peer_on;  // devices this plan's device has peer access to (pifft_allgather)
+    std::vector<hipStream_t> gst;  // pifft_allgather: one copy stream per source plan
+    std::vector<hipEvent_t> gdone;  // ... and its completion event
+    hipEvent_t gev[2] = {nullptr, nullptr};  // gather start / end on `stream`
 };
 
 namespace {
@@ -399,6 +405,11 @@ void release(pifft_plan* p) {
     if (p->d_tw) (void)hipFree(p->d_tw);
     if (p->d_hin) (void)hipFree(p->d_hin);
     if (p->d_hout) (void)hipFree(p->d_hout);
+    if (p->d_gather) (void)hipFree(p->d_gather);
+    for (auto st : p->gst) (void)hipStreamDestroy(st);
+    for (auto e : p->gdone) (void)hipEventDestroy(e);
+    for (auto e : p->gev)
+        if (e) (void)hipEventDestroy(e);
     for (auto e : p->ev) (void)hipEventDestroy(e);
     for (auto e : p->prof_ev) (void)hipEventDestroy(e);
     if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -850,12 +861,23 @@ void scatter_to_host(const pifft_plan* p, const char* res, char* host_out) {
                    res + (uint64_t)bt * p->nq * M * esz, (size_t)p->nq * M * esz);
         return;
     }
+    // a plan holding only some workers: its bins go to their stride-P
+    // natural-order positions (other positions untouched, CPU.c:496-499);
+    // typed element copies (one 8/16-B move each, not a memcpy call)
     for (uint32_t bt = 0; bt < p->batch; bt++) {
         for (uint32_t q = p->q0; q < p->q0 + p->nq; q++) {
             const uint64_t r = bitrev(q, p->lp);
-            const char* s = res + ((uint64_t)bt * p->nq * M + (uint64_t)(q - p->q0) * M) * esz;
-            char* d = host_out + ((uint64_t)bt * p->n + r) * esz;
-            for (uint64_t k = 0; k < M; k++) memcpy(d + k * p->P * esz, s + k * esz, esz);
+            const uint64_t so = (uint64_t)bt * p->nq * M + (uint64_t)(q - p->q0) * M;
+            const uint64_t d0 = (uint64_t)bt * p->n + r;
+            if (esz == 16) {
+                const cx<double>* s = reinterpret_cast<const cx<double>*>(res) + so;
+                cx<double>* d = reinterpret_cast<cx<double>*>(host_out) + d0;
+                for (uint64_t k = 0; k < M; k++) d[k * p->P] = s[k];
+            } else {
+                const cx<float>* s = reinterpret_cast<const cx<float>*>(res) + so;
+                cx<float>* d = reinterpret_cast<cx<float>*>(host_out) + d0;
+                for (uint64_t k = 0; k < M; k++) d[k * p->P] = s[k];
+            }
         }
     }
 }
@@ -863,6 +885,126 @@ void scatter_to_host(const pifft_plan* p, const char* res, char* host_out) {
 int ensure_host_staging(pifft_plan* p) {
     if (!p->d_hin) HIPCHK(hipMalloc(&p->d_hin, (size_t)p->batch * p->n * p->esz));
     if (!p->d_hout) HIPCHK(hipMalloc(&p->d_hout, (size_t)out_elems(p) * p->esz));
+    return 0;
+}
+
+int launch_interleave(const void* d_slices, void* d_out, uint64_t n, uint32_t workers, uint32_t batch, int prec,
+                      hipStream_t st) {
+    const uint64_t total = (uint64_t)batch * n;
+    const dim3 blk(256), grd(stride_grid(total));
+    const uint32_t ln = (uint32_t)ilog2u(n), lpp = (uint32_t)ilog2u(workers);
+    if (prec == PIFFT_F64)
+        hipLaunchKernelGGL(k_interleave<double>, grd, blk, 0, st, (const cx<double>*)d_slices, (cx<double>*)d_out,
+                           total, ln, lpp);
+    else if (prec == PIFFT_F32)
+        hipLaunchKernelGGL(k_interleave<float>, grd, blk, 0, st, (const cx<float>*)d_slices, (cx<float>*)d_out,
+                           total, ln, lpp);
+    else
+        return fail("bad precision");
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// The plans' worker ranges cover [0, P) exactly once, every plan slice-major
+// (PIFFT_OUT_SLICES) with the same n, P, batch and precision.
+int check_cover(pifft_plan* const* plans, int np, bool quiet) {
+    if (!plans || np <= 0) return quiet ? -1 : fail("no plans");
+    std::vector<int> order;
+    for (int i = 0; i < np; i++) {
+        const pifft_plan* p = plans[i];
+        if (!p) return quiet ? -1 : fail("plan %d is NULL", i);
+        if (p->n != plans[0]->n || p->P != plans[0]->P || p->batch != plans[0]->batch || p->prec != plans[0]->prec)
+            return quiet ? -1 : fail("plans of a gather must share n, workers, batch and precision");
+        if (p->natural || p->bitrev)
+            return quiet ? -1 : fail("plan %d: a gather needs slice-major plans (PIFFT_OUT_SLICES)", i);
+        order.push_back(i);
+    }
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return plans[a]->q0 < plans[b]->q0; });
+    uint64_t next = 0;
+    for (int i : order) {
+        if (plans[i]->q0 != next) break;
+        next += plans[i]->nq;
+    }
+    if (next != plans[0]->P)
+        return quiet ? -1 : fail("the plans' worker ranges must cover workers [0, %u) exactly once", plans[0]->P);
+    return 0;
+}
+
+// peer access from plan d's device to `src_dev` (xGMI loads/copies without a
+// host bounce); a pair that cannot peer still copies, staged by the runtime
+int enable_peer(pifft_plan* d, int src_dev) {
+    if (src_dev == d->device) return 0;
+    for (int e : d->peer_on)
+        if (e == src_dev) return 0;
+    int can = 0;
+    HIPCHK(hipDeviceCanAccessPeer(&can, d->device, src_dev));
+    if (can) {
+        const hipError_t e = hipDeviceEnablePeerAccess(src_dev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            return fail("hipDeviceEnablePeerAccess(%d -> %d): %s", d->device, src_dev, hipGetErrorString(e));
+        (void)hipGetLastError();  // clear a sticky "already enabled"
+    }
+    d->peer_on.push_back(src_dev);
+    return 0;
+}
+
+// The optional final exchange: on every destination j with
+// d_natural[j] != NULL, copy each plan's slices into the plan-owned gather
+// buffer of j's device (hipMemcpyPeerAsync over xGMI, one copy stream per
+// source so the links run concurrently), then interleave them into natural
+// order (k_interleave).  Synchronous; *ms = the slowest destination's time.
+int gather_group(pifft_plan* const* plans, int np, const void* const* d_slices, void* const* d_natural, double* ms) {
+    if (check_cover(plans, np, false)) return -1;
+    if (!d_slices || !d_natural) return fail("NULL buffer list");
+    for (int i = 0; i < np; i++)
+        if (!d_slices[i]) return fail("d_slices[%d] is NULL", i);
+    const pifft_plan* p0 = plans[0];
+    const uint64_t N = p0->n, M = p0->m;
+    const size_t esz = p0->esz;
+    for (int j = 0; j < np; j++) {
+        if (!d_natural[j]) continue;
+        pifft_plan* d = plans[j];
+        DeviceGuard g(d->device);
+        if (!d->d_gather) HIPCHK(hipMalloc(&d->d_gather, (size_t)d->batch * N * esz));
+        while ((int)d->gst.size() < np) {
+            hipStream_t st;
+            hipEvent_t ev;
+            HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            d->gst.push_back(st);
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            d->gdone.push_back(ev);
+        }
+        for (auto& e : d->gev)
+            if (!e) HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventRecord(d->gev[0], d->stream));
+        for (int i = 0; i < np; i++) {
+            const pifft_plan* s = plans[i];
+            if (enable_peer(d, s->device)) return -1;
+            hipStream_t cs = d->gst[i];
+            HIPCHK(hipStreamWaitEvent(cs, d->gev[0], 0));
+            const size_t bytes = (size_t)s->nq * M * esz;
+            for (uint32_t bt = 0; bt < d->batch; bt++) {
+                char* dst = (char*)d->d_gather + ((uint64_t)bt * N + (uint64_t)s->q0 * M) * esz;
+                const char* src = (const char*)d_slices[i] + (uint64_t)bt * bytes;
+                HIPCHK(hipMemcpyPeerAsync(dst, d->device, src, s->device, bytes, cs));
+            }
+            HIPCHK(hipEventRecord(d->gdone[i], cs));
+            HIPCHK(hipStreamWaitEvent(d->stream, d->gdone[i], 0));
+        }
+        if (launch_interleave(d->d_gather, d_natural[j], N, d->P, d->batch, d->prec, d->stream)) return -1;
+        HIPCHK(hipEventRecord(d->gev[1], d->stream));
+    }
+    double worst = 0.0;
+    for (int j = 0; j < np; j++) {
+        if (!d_natural[j]) continue;
+        pifft_plan* d = plans[j];
+        DeviceGuard g(d->device);
+        HIPCHK(hipEventSynchronize(d->gev[1]));
+        float t = 0.0f;
+        HIPCHK(hipEventElapsedTime(&t, d->gev[0], d->gev[1]));
+        worst = std::max(worst, (double)t);
+    }
+    if (ms) *ms = worst;
     return 0;
 }
 
@@ -977,10 +1119,12 @@ int pifft_profile_read(pifft_plan* p, float* launch_ms_sum, int max_launches) {
     DeviceGuard g(p->device);
     const size_t ns = p->steps.size();
     const int used = p->prof_used;
+    p->prof_steps = p->prof_used = 0;  // profiling stops, also on an error below
     std::vector<float> sum(ns, 0.0f);
-    if (used > 0) HIPCHK(hipEventSynchronize(p->prof_ev[(size_t)used * (ns + 1) - 1]));
     for (int k = 0; k < used; k++) {
         hipEvent_t* ev = &p->prof_ev[(size_t)k * (ns + 1)];
+        // each execution's end event: the executions may have run on different streams
+        HIPCHK(hipEventSynchronize(ev[ns]));
         for (size_t i = 0; i < ns; i++) {
             float ms = 0.0f;
             HIPCHK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
@@ -989,7 +1133,6 @@ int pifft_profile_read(pifft_plan* p, float* launch_ms_sum, int max_launches) {
     }
     if (launch_ms_sum)
         for (int i = 0; i < max_launches && i < (int)ns; i++) launch_ms_sum[i] = sum[i];
-    p->prof_steps = p->prof_used = 0;
     return used;
 }
 
@@ -1058,6 +1201,20 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
     if (ms1) *ms1 = t1;
     if (ms2) *ms2 = t2;
     if (host_out) {
+        if (np > 1 && check_cover(plans, np, true) == 0) {
+            // the whole transform over several plans: gather on the first
+            // plan's device (pifft_allgather; its input staging copy is free
+            // now and takes the natural-order result) and copy back once
+            std::vector<const void*> sl(np);
+            std::vector<void*> nat(np, nullptr);
+            for (int i = 0; i < np; i++) sl[i] = plans[i]->d_hout;
+            nat[0] = plans[0]->d_hin;
+            if (gather_group(plans, np, sl.data(), nat.data(), nullptr)) return -1;
+            pifft_plan* p = plans[0];
+            DeviceGuard g(p->device);
+            HIPCHK(hipMemcpy(host_out, p->d_hin, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToHost));
+            return 0;
+        }
         for (int i = 0; i < np; i++) {
             pifft_plan* p = plans[i];
             DeviceGuard g(p->device);
@@ -1090,20 +1247,12 @@ int pifft_interleave_device(const void* d_slices, void* d_out, uint64_t n, uint3
                             uint32_t batch, int prec, void* stream) {
     if (!d_slices || !d_out || d_slices == d_out) return fail("bad buffers");
     if (n < 2 || !is_pow2(n) || !workers || !is_pow2(workers) || workers > n) return fail("bad n/workers");
-    const uint64_t total = (uint64_t)batch * n;
-    const dim3 blk(256), grd(stride_grid(total));
-    hipStream_t st = (hipStream_t)stream;
-    const uint32_t ln = (uint32_t)ilog2u(n), lpp = (uint32_t)ilog2u(workers);
-    if (prec == PIFFT_F64)
-        hipLaunchKernelGGL(k_interleave<double>, grd, blk, 0, st, (const cx<double>*)d_slices, (cx<double>*)d_out,
-                           total, ln, lpp);
-    else if (prec == PIFFT_F32)
-        hipLaunchKernelGGL(k_interleave<float>, grd, blk, 0, st, (const cx<float>*)d_slices, (cx<float>*)d_out,
-                           total, ln, lpp);
-    else
-        return fail("bad precision");
-    HIPCHK(hipGetLastError());
-    return 0;
+    return launch_interleave(d_slices, d_out, n, workers, batch, prec, (hipStream_t)stream);
+}
+
+int pifft_allgather(pifft_plan* const* plans, int nplans, const void* const* d_slices, void* const* d_natural,
+                    double* ms) {
+    return gather_group(plans, nplans, d_slices, d_natural, ms);
 }
 
 int pifft_tree_device(pifft_plan* p, const void* d_in, void* d_seg, void* stream) {

@@ -832,12 +832,15 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
     const uint64_t q0 = a.q0, q1 = (uint64_t)a.q0 + a.nq;
     const uint64_t w_lo = (blk0 << L) << log_w, w_hi = ((blk0 + 1) << L) << log_w;
     if (w_hi <= q0 || w_lo >= q1) continue;  // no requested worker below this group
-    const C2* __restrict__ src = static_cast<const C2*>(a.in) + bt * a.in_bstride + base + i;
+    // no __restrict__ on src/dst: launches after the first of a multi-launch
+    // tree (log2 P > 4) run in place (src == dst == the plan's tree buffer);
+    // each thread reads and writes only its own 2^L positions
+    const C2* src = static_cast<const C2*>(a.in) + bt * a.in_bstride + base + i;
     C2 v[V];
 #pragma unroll
     for (int m = 0; m < V; m++) v[m] = src[(uint64_t)m << log_d];
     tree_levels<T, L>(v, a.tw, i, log_d, a.t0, blk0, log_w, q0, q1);
-    C2* __restrict__ dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (int64_t)(base + i) + a.out_shift;
+    C2* dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (int64_t)(base + i) + a.out_shift;
 #pragma unroll
     for (int m = 0; m < V; m++) {
         const uint64_t wm = ((blk0 << L) + m) << log_w;

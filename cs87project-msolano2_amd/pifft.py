@@ -82,6 +82,8 @@ _SIGS = {
     "pifft_tree_device": (ctypes.c_int, [_P, _P, _P, _P]),
     "pifft_profile_start": (ctypes.c_int, [_P, ctypes.c_int]),
     "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    "pifft_allgather": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                       ctypes.POINTER(ctypes.c_double)]),
 }
 SYMBOLS = tuple(_SIGS)
 
@@ -194,10 +196,8 @@ class Plan:
 
     def execute(self, host_in, host_out=None):
         """numpy in -> natural-order numpy out (only this plan's bins written)."""
-        import numpy as np
-        host_in = np.ascontiguousarray(host_in)
+        host_in, out_ptr = _host_buffers([self], host_in, host_out)
         t1, t2 = ctypes.c_double(), ctypes.c_double()
-        out_ptr = None if host_out is None else host_out.ctypes.data
         _check(lib().pifft_execute(self._h, host_in.ctypes.data, out_ptr, ctypes.byref(t1), ctypes.byref(t2)),
                "pifft_execute")
         return t1.value, t2.value
@@ -244,15 +244,62 @@ def dry_run(n: int, workers: int = 1, batch: int = 1, prec: int = F64, *, first:
     return describe_info(info)
 
 
-def execute_group(plans, host_in, host_out=None):
+def _host_buffers(plans, host_in, host_out):
+    """Checks the host arrays against the plans before any pointer crosses the
+    ABI (pifft_execute copies batch*N values from host_in and writes up to
+    batch*N values into host_out): dtype = the plans' precision (complex64 for
+    F32, complex128 for F64), at least batch*N elements, host_out C-contiguous
+    and writeable.  Returns (contiguous host_in, host_out pointer or None)."""
     import numpy as np
+    if not plans:
+        raise PifftError("no plans")
+    info = plans[0].info
+    want = np.dtype(np.complex128 if info.prec == F64 else np.complex64)
+    need = info.batch * info.n
+    host_in = np.asarray(host_in)
+    if host_in.dtype != want:
+        raise PifftError(f"host_in dtype {host_in.dtype} does not match the plan's precision ({want})")
     host_in = np.ascontiguousarray(host_in)
+    if host_in.size < need:
+        raise PifftError(f"host_in holds {host_in.size} values, the plan reads batch*N = {need}")
+    if host_out is None:
+        return host_in, None
+    if not isinstance(host_out, np.ndarray):
+        raise PifftError("host_out must be a numpy array")
+    if host_out.dtype != want:
+        raise PifftError(f"host_out dtype {host_out.dtype} does not match the plan's precision ({want})")
+    if not host_out.flags.c_contiguous or not host_out.flags.writeable:
+        raise PifftError("host_out must be C-contiguous and writeable")
+    if host_out.size < need:
+        raise PifftError(f"host_out holds {host_out.size} values, the plan writes up to batch*N = {need}")
+    return host_in, host_out.ctypes.data
+
+
+def execute_group(plans, host_in, host_out=None):
+    for p in plans[1:]:
+        if (p.info.n, p.info.batch, p.info.prec) != (plans[0].info.n, plans[0].info.batch, plans[0].info.prec):
+            raise PifftError("plans of a group must share n, batch and precision")
+    host_in, out_ptr = _host_buffers(plans, host_in, host_out)
     arr = (_P * len(plans))(*[p.handle.value for p in plans])
     t1, t2 = ctypes.c_double(), ctypes.c_double()
-    out_ptr = None if host_out is None else host_out.ctypes.data
     _check(lib().pifft_execute_group(arr, len(plans), host_in.ctypes.data, out_ptr, ctypes.byref(t1),
                                      ctypes.byref(t2)), "pifft_execute_group")
     return t1.value, t2.value
+
+
+def allgather(plans, d_slices, d_natural) -> float:
+    """pifft_allgather: every plan's slice-major result (device addresses,
+    one per plan) -> natural order on each plan's device whose d_natural entry
+    is not None.  Returns the slowest destination's time (ms)."""
+    n = len(plans)
+    if len(d_slices) != n or len(d_natural) != n:
+        raise PifftError("one slice buffer and one destination (or None) per plan")
+    arr = (_P * n)(*[p.handle.value for p in plans])
+    sl = (_P * n)(*[int(a) for a in d_slices])
+    nat = (_P * n)(*[None if a is None else int(a) for a in d_natural])
+    ms = ctypes.c_double()
+    _check(lib().pifft_allgather(arr, n, sl, nat, ctypes.byref(ms)), "pifft_allgather")
+    return ms.value
 
 
 def generate_device(d_x: int, count: int, n: int, prec: int, seed: int = 0x5EED, first: int = 0,

@@ -10,6 +10,8 @@ reference's `-n <n> -p <p> -o` interface and 5-column TSV output.
             squares of time ~ n(p-1)/p + (n/p)log2(n/p), time_tr ~ n(p-1)/p,
             time_cy ~ (n/p)log2(n/p) -- and the printout of :40-71, plus the
             empirical speedup table of :74-83.  Plots are not reproduced.
+  awk     : the reference's R-less "limited analysis" (gpu/cuda/
+            analyze-results.awk), text output identical (analyze_awk)
 
 Quirk kept on purpose: for the two-regressor fit the reference reports
 max(coef(summary(lm))[4], 1e-120), which in R's column-major indexing is the
@@ -115,6 +117,90 @@ def analyze(d: np.ndarray) -> dict:
     return res
 
 
+def _awk_num(x: float) -> str:
+    """awk's default number-to-string conversion of an array subscript
+    (integral values print as integers, others with CONVFMT %.6g)."""
+    return str(int(x)) if float(x).is_integer() else f"{x:.6g}"
+
+
+def analyze_awk(lines: list[str]) -> str:
+    """The reference's "limited analysis" (the path analyze-results takes when
+    R is absent): `awk -f analyze-results.awk results.csv | sort -n -t 1`
+    (benchmark/fourier/parallel/pi/gpu/cuda/analyze-results.awk:15-66,
+    analyze-results:27-34), restated with its quirks:
+      * rows are keyed by the whole input line (t[$0]), so identical lines
+        count once in the regression;
+      * the reported p is the largest p in STRING order (awk compares the
+        array subscripts as strings: "8" > "4" > "32" > "2" > "16" > "1");
+      * beta = sum(t law) / sum(law^2) for the combined law n(p-1)/p +
+        (n/p)log2(n/p); SS_tot is taken about the law's mean and SS_prd about
+        an uninitialised variable (0);
+      * the significance is a t-density expression, printed as 1.0e<k> with an
+        order-of-magnitude estimate below 1e-15 (floored at 1.0e-120);
+      * `sort -n -t 1` puts the text lines (numeric value 0, byte order) before
+        the table rows (ascending n)."""
+    n_obs, p_obs, t_sum, t, t_law = {}, {}, {}, {}, {}
+    nr = 0
+
+    def law(n, p):
+        return n * ((p - 1) / p) + (n / p) * (math.log(n / p) / math.log(2))
+
+    for ln in lines:
+        f = ln.split()
+        if not f:
+            continue
+        nr += 1
+        n, p, tm = float(f[0]), float(f[1]), float(f[2])
+        kn, kp = _awk_num(n), _awk_num(p)
+        n_obs[kn], p_obs[kp] = n, p
+        t_sum[(kn, kp)] = t_sum.get((kn, kp), 0.0) + tm
+        key = ln.rstrip("\n")
+        t[key], t_law[key] = tm, law(n, p)
+    K = nr / (len(n_obs) * len(p_obs))
+    at_a = sum(t_law[i] * t_law[i] for i in t)
+    at_b = sum(t[i] * t_law[i] for i in t)
+    beta = at_b / at_a
+    N = len(t)
+    t_law_m = sum(t_law.values()) / N
+    ss_res = sum((t[i] - beta * t_law[i]) ** 2 for i in t)
+    ss_prd = sum((t_law[i] - 0.0) ** 2 for i in t)
+    eta = N - 2
+    t_score = beta * math.sqrt(eta) / math.sqrt(ss_res / ss_prd)
+    a = 1 / math.sqrt(eta)
+    if eta % 2 == 0:
+        a /= 2
+        e = eta - 1
+        while e > 2:
+            a *= e / (e - 1)
+            e -= 2
+    else:
+        a /= math.atan2(0, -1)
+        e = eta - 1
+        while e > 1:
+            a *= e / (e - 1)
+            e -= 2
+    try:
+        a /= math.sqrt(1 + t_score ** 2 / eta) ** eta
+    except OverflowError:  # awk's ^ overflows to inf, and a / inf = 0
+        a = 0.0
+    pi = max(p_obs, key=lambda k: k)  # string order
+    out = [f"Empirical time complexity of pi-DFT on NVIDIA GPU (p={int(float(pi))}, {int(K)} replications):"]
+    if a < 1e-15:
+        a_exp = int(42.480516 - 1.216025 * t_score - 1.366767 * eta)
+        out.append(f"Fit significant at the alpha < 1.0e{max(a_exp, -120)} level.")
+    else:
+        out.append(f"Fit significant at the alpha < {a:.2e} level.")
+    out.append("Input size (n)\tAvg. time (ms)\tTheta(n(p-1)/p + (n/p)log(n/p))")
+    for kn, n in n_obs.items():
+        out.append("%u\t\t%.2f\t\t%.2f" % (int(n), t_sum.get((kn, pi), 0.0) / K, beta * law(n, p_obs[pi])))
+
+    def sort_key(line):
+        import re
+        m = re.match(r"\s*[-+]?\d+(\.\d*)?", line)
+        return (float(m.group(0)) if m else 0.0, line.encode())
+    return "\n".join(sorted(out, key=sort_key)) + "\n"
+
+
 def report(res: dict) -> str:
     out = []
     out.append("  Testing the hypothesis that the parallel time complexity follows the law\n"
@@ -151,7 +237,13 @@ def main(argv=None) -> int:
     r.add_argument("extra", nargs="*")
     a = sub.add_parser("analyze")
     a.add_argument("results")
+    w = sub.add_parser("awk")
+    w.add_argument("results")
     args = ap.parse_args(argv)
+    if args.cmd == "awk":
+        with open(args.results) as f:
+            sys.stdout.write(analyze_awk(f.readlines()))
+        return 0
     if args.cmd == "run":
         if args.T <= 0:
             print("Invalid number of replications!")

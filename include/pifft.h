@@ -118,7 +118,11 @@ int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
 
 /* Device boundary: d_in holds info.in_elems complex values, d_out receives
  * info.out_elems (d_in != d_out; neither is freed).  Asynchronous on `stream`
- * (a hipStream_t; NULL = the default stream, as in other ROCm libraries). */
+ * (a hipStream_t; NULL = the default stream, as in other ROCm libraries).
+ * A plan owns its workspace (ping-pong and tree buffers): it must not execute
+ * concurrently with itself -- two executions of one plan on different streams
+ * race on that workspace.  Use one plan per stream (the reference gives each
+ * worker its own scratch, CPU.c:396-404). */
 int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* stream);
 
 /* As pifft_execute_device, but records a HIP event before every launch and
@@ -130,10 +134,10 @@ int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, 
 /* Asynchronous per-launch timing: after pifft_profile_start(plan, steps),
  * each of the next `steps` pifft_execute_device calls records a HIP event
  * before every launch and after the last one on its stream (no host sync);
- * pifft_profile_read waits for the last recorded event, writes the per-launch
- * duration summed over the recorded executions to launch_ms_sum[0 ..
- * min(num_launches, max_launches)), stops profiling and returns the number of
- * executions recorded (or -1). */
+ * pifft_profile_read waits for every recorded execution's last event, writes
+ * the per-launch duration summed over the recorded executions to
+ * launch_ms_sum[0 .. min(num_launches, max_launches)), stops profiling (also
+ * when it fails) and returns the number of executions recorded (or -1). */
 int pifft_profile_start(pifft_plan* plan, int steps);
 int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int max_launches);
 
@@ -143,15 +147,38 @@ int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int max_launches)
  * positions untouched -- the reference's workers write disjoint `out` entries,
  * CPU.c:496-499).  A PIFFT_OUT_BITREV plan instead writes its workers'
  * scratch segments at host_out[b N + q M + i] (the reference's tmp_in
- * layout, q = first..first+count-1).  ms_stage1 / ms_stage2 receive the device time of the tree
- * stage and of the rest (the reference's two timers, CPU.c:414-481). */
+ * layout, q = first..first+count-1).  ms_stage1 / ms_stage2 receive the
+ * device time of the tree stage and of the rest (the reference's two timers,
+ * CPU.c:414-481).  When a plan evaluates its tree inside the first local-FFT
+ * pass (one worker per plan, log2 P <= 4, a multi-pass local FFT; see
+ * pifft_plan_info.launch_kind 4) that fused launch cannot be split: stage 1 is
+ * then the tree PLUS the first pass, and stage 2 the remaining passes. */
 int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double* ms_stage1,
                   double* ms_stage2);
 
 /* Several plans (normally one per GPU) run concurrently from one host thread:
- * the P-GPU no-communication split.  Stage times are the max over plans. */
+ * the P-GPU no-communication split.  Stage times are the max over plans.
+ * When the plans hold all P workers between them (PIFFT_OUT_SLICES), host_out
+ * is filled through pifft_allgather onto the first plan's device and one
+ * device-to-host copy; otherwise each plan's bins are scattered on the host. */
 int pifft_execute_group(pifft_plan** plans, int nplans, const void* host_in, void* host_out,
                         double* ms_stage1, double* ms_stage2);
+
+/* The optional final exchange of a multi-GPU job (the
+ * reference's counterpart is every worker writing its bins into the shared
+ * natural-order `out`, CPU.c:496-499).  plans[i] holds workers
+ * [first_i, first_i + count_i) with its slice-major result at d_slices[i] (on
+ * plan i's device, PIFFT_OUT_SLICES layout, e.g. the d_out of its
+ * pifft_execute_device); between them the plans must cover all P workers
+ * exactly once.  For every j with d_natural[j] != NULL, each plan's slices are
+ * copied to plan j's device (hipMemcpyPeerAsync over xGMI, one copy stream per
+ * source; a device-local copy when both share a device) and interleaved there
+ * into natural order: d_natural[j] receives batch*N values.  Call it once the
+ * executions that produced d_slices have completed.  Synchronous; ms (may be
+ * NULL) receives the slowest destination's copy + interleave time.  Uses a
+ * plan-owned batch*N gather buffer on each destination device. */
+int pifft_allgather(pifft_plan* const* plans, int nplans, const void* const* d_slices, void* const* d_natural,
+                    double* ms);
 
 /* Synthetic input on the device: element e (count of them, starting at global
  * element index `first`) = splitmix64(seed) draws 2e, 2e+1 mapped to

@@ -22,11 +22,11 @@ def _bench(*args):
     return json.loads(lines[0])
 
 
-def _common(d, steps, warmup):
+def _common(d, steps, warmup, n_gpus=1):
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert d["metric"] == json.load(f)["metric"]
     assert d["unit"] == "GFLOP/s" and d["higher_is_better"] is True
-    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == warmup
+    assert d["n_gpus"] == n_gpus and d["steps"] == steps and d["warmup"] == warmup
     assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["scaling"] in ("strong", "weak") and d["vs_baseline"] is None
     n = d["config"]["n"]
@@ -56,3 +56,33 @@ def test_bench_batch_shard_rank_share():
     _common(d, 3, 1)
     assert d["dtype"] == "f32" and d["config"]["batch_per_gpu"] == 16 and d["config"]["shard"] == "batch"
     assert d["cpu_baseline"] is None  # emulated rank: never a job-level CPU comparison
+
+
+def test_bench_gpus_2_spawns_two_ranks():
+    """--gpus 2 without torchrun launches two rank processes (rehearsed on one
+    GPU with gloo): n_gpus 2, one record per rank, the all-gather timed."""
+    d = _bench("--gpus", "2", "--same-device", "--dist-backend", "gloo", "--log-n", "20", "--steps", "3",
+               "--warmup", "1")
+    _common(d, 3, 1, n_gpus=2)
+    pr = d["config"]["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1] and [r["workers"] for r in pr] == [[0, 1], [1, 2]]
+    assert all(r["ms_per_step"] > 0 and 0 < r["frac"] for r in pr)
+    # the job time is the slowest rank's
+    assert d["ms_per_step"] >= max(r["ms_per_step"] for r in pr) * 0.999
+    assert d["config"]["allgather_ms"] > 0 and d["cpu_baseline"] is None
+
+
+def test_bench_secondary_configs():
+    """The headline run also times configs 1, 2 (whole + one slice) and 3, each
+    with its own dominant-kernel roofline (CPU baselines skipped here)."""
+    d = _bench("--steps", "2", "--warmup", "1", "--no-cpu-baseline")
+    _common(d, 2, 1)
+    sec = d["config"]["secondary"]
+    assert set(sec) == {"C1", "C2", "C2_slice", "C3"}
+    for key, rec in sec.items():
+        assert "error" not in rec, (key, rec)
+        flops = 5.0 * rec["n"] * (rec["n"].bit_length() - 1) * rec["batch"]
+        assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= rec["value"] * 1e-3 + 0.01
+        assert 0 < rec["roofline"]["frac"] < 1.2
+    assert sec["C3"]["dtype"] == "f32" and sec["C3"]["batch"] == 4096
+    assert sec["C2"]["workers"] == 8 and sec["C2_slice"]["workers_in_plan"] == 1

@@ -3,7 +3,8 @@
 Oracle: the reference's own outputs (tests/golden/, bitwise-pinned) and the C
 restatement (oracle/) on the same seeded inputs.  Bars (BASELINE.json
 north_star): relative L2 error <= 1e-12 (fp64) and <= 1e-5*log2(N) (fp32);
-index permutation exact (checked per bin as well as in L2); the tree stage
+index permutation exact (every bin within 50 x the tolerance of the typical
+bin magnitude of its own reference value, as well as in L2); the tree stage
 and the input generator bit-exact.  Sizes beyond the oracle's reach are checked
 through size-independent properties (double-transform identity, Parseval,
 linearity, direct DFT bins, P-split consistency).
@@ -49,10 +50,12 @@ def run(plan, x, slices=False):
 def assert_bins_close(got, want, suf, n):
     err = rel_l2(got, want)
     assert err <= tol(suf, n), f"rel-L2 {err:.3e} > {tol(suf, n):.1e}"
-    # permutation: every bin must be closer to its own reference value than the
-    # spread of the spectrum (a swapped index would show as an O(1) error)
-    scale = np.linalg.norm(want) / math.sqrt(len(want))
-    assert np.max(np.abs(got - want)) <= max(50 * tol(suf, n), 1e-9) * scale * math.sqrt(len(want))
+    # permutation, per bin: every bin within 50 tol of the TYPICAL bin
+    # magnitude rms(X) = ||X|| / sqrt(N) of its own reference value (a
+    # misplaced bin is off by ~rms; at fp32 2^26 the bound is 1.3 % of rms)
+    rms = np.linalg.norm(want) / math.sqrt(len(want))
+    worst = float(np.max(np.abs(got - want)))
+    assert worst <= max(50 * tol(suf, n), 1e-9) * rms, f"bin error {worst:.3e} vs rms {rms:.3e}"
 
 
 def test_device_visible():
@@ -479,8 +482,9 @@ def test_config5_one_worker_of_8_n2e32():
 # ------------------------------------------- the reference's run(), patched ---
 def _ref_gpu(prec):
     p = os.path.join(oracle.REF_DIR, "fourier-parallel-pi-cpu-pthreads-gpu" + ("-f64" if prec == 64 else ""))
-    if not os.path.exists(p):
-        pytest.skip("oracle/_ref integration binary not built (make -C oracle ref-gpu)")
+    # built in the build container (__graft_entry__.build) and shipped with the
+    # tree: its absence on the GPU box is a failure, not a skip
+    assert os.path.exists(p), "oracle/_ref integration binary not built (make -C oracle ref-gpu)"
     return p
 
 
@@ -629,3 +633,133 @@ def test_chunked_pass_pair_config4_bitwise(monkeypatch):
     plain.execute_device(x.data_ptr(), b.data_ptr(), torch.cuda.current_stream())
     torch.cuda.synchronize()
     assert torch.equal(torch.view_as_real(a), torch.view_as_real(b))
+
+
+# ------------------------------------------------ the final exchange (8e) ---
+@pytest.mark.parametrize("suf,logn,P,per,batch", [("f64", 20, 8, 1, 1), ("f32", 18, 8, 2, 3), ("f64", 16, 4, 1, 2),
+                                                  ("f64", 12, 64, 16, 1)])
+def test_allgather_bitwise_vs_host_scatter(suf, logn, P, per, batch):
+    """pifft_allgather over the plans of a P-worker split (all on this GPU;
+    hipMemcpyPeerAsync degenerates to a device copy) equals the host-side
+    interleave of the same slices bit for bit, and the natural-order transform
+    within tolerance."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn)
+    d_in = dev(x)
+    st = torch.cuda.current_stream()
+    plans = [pifft.Plan(n, P, batch, PREC[suf], first=f, count=per, device=0) for f in range(0, P, per)]
+    slices = [torch.empty(p.info.out_elems, dtype=d_in.dtype, device="cuda") for p in plans]
+    for p, s in zip(plans, slices):
+        p.execute_device(d_in.data_ptr(), s.data_ptr(), st)
+    torch.cuda.synchronize()
+    nat = torch.empty(n * batch, dtype=d_in.dtype, device="cuda")
+    ms = pifft.allgather(plans, [s.data_ptr() for s in slices], [nat.data_ptr()] + [None] * (len(plans) - 1))
+    assert ms > 0
+    got = nat.cpu().numpy().reshape(batch, n)
+    host = [s.cpu().numpy().reshape(batch, per, n // P) for s in slices]
+    for bt in range(batch):
+        sl = np.concatenate([h[bt] for h in host])  # (P, M), worker order
+        assert got[bt].tobytes() == pifft_dist.interleave_slices(sl).tobytes()
+        want = oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8)
+        assert_bins_close(got[bt], want, suf, n)
+    # every destination gets the same result
+    if len(plans) > 1:
+        nat2 = torch.empty_like(nat)
+        dests = [None] * len(plans)
+        dests[-1] = nat2.data_ptr()
+        pifft.allgather(plans, [s.data_ptr() for s in slices], dests)
+        torch.cuda.synchronize()
+        assert torch.equal(nat2, nat)
+
+
+def test_allgather_errors():
+    n, P = 1 << 12, 4
+    plans = [pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0) for q in range(P)]
+    bufs = [torch.empty(n // P, dtype=torch.complex128, device="cuda") for _ in range(P)]
+    nat = torch.empty(n, dtype=torch.complex128, device="cuda")
+    with pytest.raises(pifft.PifftError, match="cover workers"):
+        pifft.allgather(plans[:3], [b.data_ptr() for b in bufs[:3]], [nat.data_ptr(), None, None])
+    with pytest.raises(pifft.PifftError, match="cover workers"):
+        dup = [plans[0], plans[0], plans[2], plans[3]]
+        pifft.allgather(dup, [b.data_ptr() for b in bufs], [nat.data_ptr(), None, None, None])
+    whole = pifft.Plan(n, P, 1, pifft.F64)
+    with pytest.raises(pifft.PifftError, match="slice-major"):
+        pifft.allgather([whole], [bufs[0].data_ptr()], [nat.data_ptr()])
+    other = pifft.Plan(n * 2, P, 1, pifft.F64, first=3, count=1, device=0)
+    with pytest.raises(pifft.PifftError, match="share"):
+        pifft.allgather(plans[:3] + [other], [b.data_ptr() for b in bufs], [nat.data_ptr(), None, None, None])
+
+
+@pytest.mark.parametrize("suf", list(DT))
+def test_execute_group_device_gather_equals_host_scatter(suf):
+    """pifft_execute_group: a group holding all workers returns host_out via
+    the device gather; the same plans run as partial groups scatter on the
+    host.  Both paths give the same bytes (and the transform)."""
+    n, P, batch = 1 << 16, 8, 2
+    x = oracle.generate(n * batch, DT[suf], seed=99)
+    plans = [pifft.Plan(n, P, batch, PREC[suf], first=q, count=1, device=0) for q in range(P)]
+    a = np.zeros(n * batch, dtype=DT[suf])
+    pifft.execute_group(plans, x, a)
+    b = np.zeros(n * batch, dtype=DT[suf])
+    pifft.execute_group(plans[:3], x, b)  # partial groups: host scatter
+    pifft.execute_group(plans[3:], x, b)
+    assert a.tobytes() == b.tobytes()
+    for bt in range(batch):
+        assert_bins_close(a[bt * n:(bt + 1) * n], oracle.fft(x[bt * n:(bt + 1) * n], P=1), suf, n)
+
+
+def test_host_boundary_rejects_mismatched_buffers():
+    """Plan.execute checks dtype, size, contiguity and writeability before any
+    pointer crosses the ABI (a wrong buffer would be read/written out of
+    bounds by the C side)."""
+    n = 1024
+    plan = pifft.Plan(n, 2, 1, pifft.F64)
+    x = oracle.generate(n, np.complex128)
+    with pytest.raises(pifft.PifftError, match="dtype"):
+        plan.execute(x.astype(np.complex64), np.zeros(n, np.complex128))
+    with pytest.raises(pifft.PifftError, match="dtype"):
+        plan.execute(x, np.zeros(n, np.complex64))
+    with pytest.raises(pifft.PifftError, match="holds"):
+        plan.execute(x[: n // 2], np.zeros(n, np.complex128))
+    with pytest.raises(pifft.PifftError, match="holds"):
+        plan.execute(x, np.zeros(n // 2, np.complex128))
+    with pytest.raises(pifft.PifftError, match="contiguous"):
+        plan.execute(x, np.zeros(2 * n, np.complex128)[::2])
+    ro = np.zeros(n, np.complex128)
+    ro.setflags(write=False)
+    with pytest.raises(pifft.PifftError, match="writeable"):
+        plan.execute(x, ro)
+    out = np.zeros(n, np.complex128)
+    plan.execute(x, out)
+    assert_bins_close(out, oracle.fft(x, P=2), "f64", n)
+
+
+# -------------------------------------------------------------- 8(f) rows ---
+def test_cli_lists_devices():
+    """-l: the device query (the reference's how-many-concurrent-blocks /
+    how_many_cores, gpu/cuda/how-many-concurrent-blocks.cu:65, CPU.c:835-837)."""
+    r = _cli(["-l"])
+    assert r.returncode == 0, r.stderr
+    assert int(r.stdout.strip()) == pifft.gpu_count() >= 1
+
+
+@pytest.mark.timeout(300)
+def test_sweep_drives_the_mi355x_cli(tmp_path):
+    """8(f) row 1 on the GPU: the reference's experiment loop (T x n x p ->
+    5-column TSV, gpu/cuda/run-experiments:58-66) over the MI355X CLI, fed to
+    both of the reference's analyses (analyze-results.R:35-71 regressions and
+    the R-less analyze-results.awk)."""
+    import pifft_sweep
+    out = tmp_path / "mi355x.tsv"
+    k = pifft_sweep.run_sweep(pifft.CLI_PATH, 2, 1 << 16, 1 << 20, 1, 8, str(out), extra=["-f", "64", "-s", "5"])
+    d = pifft_sweep.load(str(out))
+    assert k == len(d) == 2 * 5 * 4
+    assert set(d[:, 0]) == {1 << e for e in range(16, 21)} and set(d[:, 1]) == {1, 2, 4, 8}
+    assert np.all(d[:, 2] > 0) and np.allclose(d[:, 2], d[:, 3] + d[:, 4], atol=2e-3)
+    assert np.all(d[d[:, 1] == 1][:, 3] == 0)  # P = 1: no tree stage
+    res = pifft_sweep.analyze(d)
+    assert np.all(np.isfinite(res["coef_time"])) and set(res["speedup"]) == set(int(v) for v in d[:, 0])
+    txt = pifft_sweep.analyze_awk(out.read_text().splitlines(keepends=True))
+    lines = txt.splitlines()
+    assert lines[0].startswith("Empirical time complexity of pi-DFT on NVIDIA GPU (p=8, 2 replications)")
+    assert [int(ln.split()[0]) for ln in lines[3:]] == [1 << e for e in range(16, 21)]

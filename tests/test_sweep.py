@@ -41,10 +41,33 @@ def test_law_fit_recovers_coefficients():
 def test_run_sweep_with_reference_binary(tmp_path):
     exe = oracle.reference_binary(32)
     if not exe:
-        pytest.skip("oracle/_ref not built")
+        pytest.fail("oracle/_ref not built (make -C oracle ref): the sweep check needs the reference binary")
     out = tmp_path / "r.tsv"
     k = pifft_sweep.run_sweep(exe, 2, 1024, 4096, 1, 4, str(out), max_p=os.cpu_count())
     d = pifft_sweep.load(str(out))
     assert k == len(d) == 2 * 3 * 3
     assert set(d[:, 0]) == {1024, 2048, 4096} and set(d[:, 1]) == {1, 2, 4}
     assert np.allclose(d[:, 2], d[:, 3] + d[:, 4], atol=1e-3)
+
+
+@pytest.mark.parametrize("name", ["ref_cuda_results", "ref_xeonphi_results", "syn_results"])
+def test_awk_limited_analysis_reproduced(name):
+    """The reference's R-less analysis (gpu/cuda/analyze-results.awk piped
+    through `sort -n -t 1`), text-identical to its output on the reference's
+    committed CUDA and Xeon Phi results and on a synthetic file exercising its
+    quirks (fixtures: tests/golden/gen_awk_golden.py)."""
+    with open(os.path.join(GOLDEN, name + ".tsv")) as f:
+        lines = f.readlines()
+    with open(os.path.join(GOLDEN, f"awk_{name}.txt")) as f:
+        want = f.read()
+    assert pifft_sweep.analyze_awk(lines) == want
+
+
+def test_reference_cuda_results_fit():
+    """The reference's CUDA results file through the R-path regressions: its
+    stage-1 and stage-2 times follow the law (the stage fits are significant)."""
+    d = pifft_sweep.load(os.path.join(GOLDEN, "ref_cuda_results.tsv"))
+    assert d.shape == (240, 5) and set(d[:, 0]) == {1024, 2048, 4096, 8192} and set(d[:, 1]) == {1, 2, 4, 8, 16, 32}
+    res = pifft_sweep.analyze(d)
+    assert res["alpha_tr"] < 1e-6 and res["alpha_cy"] < 1e-6
+    assert res["speedup"][8192][32] > 10  # 102.8 -> 7.7 ms (SURVEY.md section 6)
