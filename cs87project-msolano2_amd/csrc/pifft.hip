@@ -106,9 +106,10 @@ const std::vector<PassKernel>& pass_kernels() {
     return all;
 }
 
-const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0) {
+const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0, int vpt = 16) {
     for (const auto& k : pass_kernels())
-        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp) return &k;
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt)
+            return &k;
     return nullptr;
 }
 
@@ -148,7 +149,7 @@ struct pifft_plan {
     std::vector<Step> tree_only;  // the tree stage alone, for pifft_tree_device
     std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: steps x (launches + 1)
     int prof_steps = 0, prof_used = 0;
-    int radix[8] = {0}, lines[8] = {0};
+    int radix[8] = {0}, lines[8] = {0}, vpt[8] = {0};
     void* buf[NBUF] = {nullptr};
     size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0, bytes_ch = 0;
     int chunk_pairs = 0;  // chunked last-two-pass pairs (one per chunk)
@@ -246,6 +247,7 @@ TwoLevel two_level(TableBuilder& tb, uint64_t L) {
 
 struct PassChoice {
     int R, C, mode, nts;
+    int vpt = 16;
 };
 
 // Tile = R x C elements per workgroup (C adjacent lines of an R-point sub-FFT).
@@ -313,6 +315,14 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         const int R = (int)M;
         const int C = pick_lines(prec, R, ntrans, ntrans, prec == 64 ? "PIFFT_SINGLE_C64" : "PIFFT_SINGLE_C32", 0);
         if (!find_pass(prec, R, C, 0, nts)) return fail("no pass kernel for R=%d C=%d", R, C);
+        // tuning: 8 values per thread (radix-8 stages, twice the waves per
+        // sub-FFT) -- measured slower than 16 at every batch size
+        // (profiles/r02_vpt_sweep.log), so only on request and if instantiated
+        const int vpt = env_int("PIFFT_SINGLE_VPT", 16);
+        if (vpt != 16 && find_pass(prec, R, C, 0, nts, 0, vpt)) {
+            out.push_back({R, C, 0, nts, vpt});
+            return 0;
+        }
         out.push_back({R, C, 0, nts});
         return 0;
     }
@@ -520,8 +530,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
         PassChoice& l = passes.back();
         const int bm = l.mode, cmin = bm == 0 ? 1 : 4;
         int C = l.C;
-        while (C > cmin && !find_pass(p->prec, l.R, C, bm | 4, l.nts)) C /= 2;
-        if (!find_pass(p->prec, l.R, C, bm | 4, l.nts))
+        while (C > cmin && !find_pass(p->prec, l.R, C, bm | 4, l.nts, 0, l.vpt)) C /= 2;
+        if (!find_pass(p->prec, l.R, C, bm | 4, l.nts, 0, l.vpt))
             return fail("no bit-reversed pass kernel R=%d C=%d mode=%d", l.R, l.C, bm);
         l.C = C;
         l.mode = bm | 4;
@@ -638,7 +648,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         const int last_nt = last_pass && passes[i].mode == 2 ? env_int("PIFFT_LAST_NT", -1) : -1;
         const PassKernel* k = fuse_here ? fused
                                         : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode,
-                                                    last_nt >= 0 ? last_nt : passes[i].nts);
+                                                    last_nt >= 0 ? last_nt : passes[i].nts, 0, passes[i].vpt);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
@@ -679,6 +689,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         if (i < 8) {
             p->radix[i] = k->R;
             p->lines[i] = k->C;
+            p->vpt[i] = k->vpt;
         }
         ns *= (uint64_t)k->R;
         Elem e;
@@ -1072,6 +1083,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     for (int i = 0; i < 8; i++) {
         info->radix[i] = p->radix[i];
         info->lines[i] = p->lines[i];
+        info->vpt[i] = p->vpt[i];
     }
     std::vector<const void*> fns;
     for (size_t i = 0; i < p->steps.size() && i < PIFFT_MAX_LAUNCH_INFO; i++) {

@@ -396,24 +396,25 @@ __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, u
     return ((uint64_t)(slot >> log_xg) << (log_xg + 3)) + ((uint64_t)xcd << log_xg) + (slot & gmask);
 }
 
-// values held per thread (VPT).  16 for both precisions: 32 fp32 values (the
-// same bytes as 16 fp64) measured 160-200 VGPRs with spills at 128.
-template <typename T>
-constexpr int vpt_of() { return 16; }  // 32 for fp32 measured: 160-200 VGPRs, spills
-
+// values held per thread (VPT, a k_pass template argument): 16 for both
+// precisions (32 fp32 values -- the same bytes as 16 fp64 -- measured 160-200
+// VGPRs with spills at 128; 8 -- radix-8 stages, twice the waves per sub-FFT --
+// measured slower for every single-pass batch size, profiles/r02_vpt_sweep.log).
+// VPT 16: radix-16 stages + one trailing radix 2/4/8/16 stage; VPT 8: radix-8
+// stages + one trailing radix 2/4/8.
 template <int R, int VPT = 16>
 struct PassShape {
     static constexpr int Q = R >= VPT ? VPT : (R >= 16 ? 16 : R);  // values per thread
+    static constexpr int B = Q >= 16 ? 16 : Q;                      // radix of the non-last stages
+    static constexpr int LOGB = ilog2c(B);
     static constexpr int LOGR = ilog2c(R);
-    static constexpr int NSTG = (LOGR + 3) / 4;              // radix-16 stages + 1 trailing
-    static constexpr int QL = 1 << (LOGR - 4 * (NSTG - 1));  // trailing radix 2/4/8/16
-    static constexpr int LS = R + R / 16 + 1;                // LDS line stride (odd, scalars)
+    static constexpr int NSTG = LOGB ? (LOGR + LOGB - 1) / LOGB : 1;   // radix-B stages + 1 trailing
+    static constexpr int QL = 1 << (LOGR - LOGB * (NSTG - 1));        // trailing radix
 };
 
 template <int R, int C, int VPT = 16>
 struct PassCfg {
     static constexpr int NT = C * R / PassShape<R, VPT>::Q;
-    static constexpr int lds_elems = PassShape<R, VPT>::NSTG > 1 ? C * PassShape<R, VPT>::LS : 0;  // scalars
 #ifndef PIFFT_MIN_WG_PER_CU
 #define PIFFT_MIN_WG_PER_CU 2
 #endif
@@ -423,7 +424,38 @@ struct PassCfg {
     static constexpr int waves_per_eu = wpe > 4 ? 4 : wpe;
 };
 
-__device__ __forceinline__ int lds_pad(int r) { return r + (r >> 4); }
+// LDS image of a workgroup's C lines during an exchange (one component, T
+// scalars): element r of line c sits at c*ls + swz(r), swz(r) = (r XOR ((r >>
+// xs) & xm) XOR ((c & cm) << cs)) + (ps ? r >> ps : 0) -- XOR swizzles of the
+// low bits (by higher bits of r, or by the line) and/or one pad scalar per 2^ps.  The round-1 layout (lds_default: r + r/16, odd line
+// stride) had 2-way bank conflicts on every exchange of the C4 first pass
+// (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.40, profiles/r01_lds_pmc.txt).
+// tools/lds_model.hip replays each pass instance's exchanges through the
+// kernel's own thread maps (Stage::map) under the gfx950 banking rules
+// (MI355X_MICROARCH.md, LDS) and picks, per instance, the layout with the
+// fewest LDS-array cycles at no more LDS than the default: the generated
+// LdsPick specializations in pifft_lds_layouts.inc.
+struct LdsLayout {
+    int ls, xs, xm, ps, cm, cs;  // (cm, cs): XOR of (c & cm) << cs, a per-line rotation of the banks
+};
+__host__ __device__ constexpr int lds_at(LdsLayout L, int c, int r) {
+    return c * L.ls + (r ^ ((r >> L.xs) & L.xm) ^ ((c & L.cm) << L.cs)) + (L.ps ? (r >> L.ps) : 0);
+}
+template <int R>
+constexpr LdsLayout lds_default() { return LdsLayout{R + R / 16 + 1, 4, 0, 4, 0, 0}; }
+template <typename T, int R, int C, int BM, int VPT>
+struct LdsPick {
+    static constexpr LdsLayout value = lds_default<R>();
+};
+#ifndef PIFFT_LDS_DEFAULT_ONLY
+#include "pifft_lds_layouts.inc"
+#endif
+
+// dynamic LDS bytes of a k_pass instance (0 for a single-stage sub-FFT)
+template <typename T, int R, int C, int MODE, int VPT>
+constexpr int pass_lds_bytes() {
+    return PassShape<R, VPT>::NSTG > 1 ? C * LdsPick<T, R, C, MODE & 3, VPT>::value.ls * (int)sizeof(T) : 0;
+}
 
 // v[k] *= w^k (0 < k < q), w^k = w^(k - lowbit k) * w^(lowbit k), anchors
 // a[i] = w^(2^i): chains of <= 3 products, each power applied when formed.
@@ -449,10 +481,10 @@ struct Stage {
     using Sh = PassShape<R, VPT>;
     static constexpr int NT = PassCfg<R, C, VPT>::NT;
     static constexpr bool first = S == 0, last = S == Sh::NSTG - 1;
-    static constexpr int q = last ? Sh::QL : 16;
+    static constexpr int q = last ? Sh::QL : Sh::B;
     static constexpr int U = Sh::Q / q;
     static constexpr int NB = R / q;
-    static constexpr int ns = 1 << (4 * S);
+    static constexpr int ns = 1 << (Sh::LOGB * S);
     static constexpr bool cfast = first ? (MODE != 0) : (last ? (MODE == 2) : false);  // MODE 3 as MODE 1
 #ifndef PIFFT_WAVE_PRIVATE
 #define PIFFT_WAVE_PRIVATE 3  // bit 0: whole-line stages (a), bit 1: beta groups (b)
@@ -493,7 +525,7 @@ struct Stage {
     static constexpr bool perm = last && !first && !cfast && Sh::Q == 16 && NT % 64 == 0 && Sh::NSTG == 3 &&
                                  (((PIFFT_PERMLANE & 2) && q == 4 && NBP == 64) ||
                                   ((PIFFT_PERMLANE & 1) && q == 2 && NBP == 32));
-    __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
+    __host__ __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
         if constexpr (perm) {
             const int lane = tid & 63;
             c = (tid >> 6) * (64 / NBP) + lane / NBP;
@@ -563,10 +595,9 @@ __device__ __forceinline__ void pl_swap(cx<T>& a, cx<T>& b) {
     __builtin_memcpy(&b, y, sizeof b);
 }
 
-template <typename T, int R, int C, int MODE, int NTS, int LP, int S>
+template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
     using C2 = cx<T>;
-    constexpr int VPT = vpt_of<T>();
     // MODE | 4: the same pass storing at bitrev_{log2 M}(natural position),
     // the reference's scratch order (PIFFT_OUT_BITREV; last pass only).  Each
     // line's R outputs still land in one contiguous R-element block; plain
@@ -576,7 +607,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     constexpr bool BREV = (MODE & 4) != 0;
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
-    constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns, LS = Sh::LS;
+    constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
+    constexpr LdsLayout LL = LdsPick<T, R, C, BM, VPT>::value;
     // (run-time even where the mode fixes them -- M/R = 1 for a single pass,
     // Ns = 1 for a first pass: compile-time values measured 2 % slower there)
     const uint32_t log_lb = a.log_lb;
@@ -739,7 +771,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #pragma unroll
             for (int g = 0; g < 8; g++) pl_swap<16>(v[2 * g], v[2 * g + 1]);
         }
-        pass_stages<T, R, C, MODE, NTS, LP, S + 1>(a, lds, v, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, tid, tile);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
         using Nx = Stage<R, C, BM, S + 1, VPT>;
@@ -753,7 +785,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 St::map(tid, u, c, b);
                 const int base = (b / ns) * ns * q + (b & (ns - 1));  // r' = base + k ns
 #pragma unroll
-                for (int k = 0; k < q; k++) lds[c * LS + lds_pad(base + k * ns)] = comp ? v[u * q + k].im : v[u * q + k].re;
+                for (int k = 0; k < q; k++) lds[lds_at(LL, c, base + k * ns)] = comp ? v[u * q + k].im : v[u * q + k].re;
             }
             lds_handoff<Nx::wave_private>();
 #pragma unroll
@@ -762,12 +794,12 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 Nx::map(tid, u, c, b);
 #pragma unroll
                 for (int k = 0; k < Nx::q; k++) {
-                    const T x = lds[c * LS + lds_pad(b + k * Nx::NB)];
+                    const T x = lds[lds_at(LL, c, b + k * Nx::NB)];
                     if (comp) v[u * Nx::q + k].im = x; else v[u * Nx::q + k].re = x;
                 }
             }
         }
-        pass_stages<T, R, C, MODE, NTS, LP, S + 1>(a, lds, v, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, tid, tile);
     }
 }
 
@@ -778,18 +810,18 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
 // NTS: non-temporal streaming of the data (nt_loads / nt_stores)
-template <typename T, int R, int C, int MODE, int NTS, int LP>
-__global__ __launch_bounds__((PassCfg<R, C, vpt_of<T>()>::NT),
-                             (MODE == 3 && LP >= 4 && PassCfg<R, C, vpt_of<T>()>::waves_per_eu > 2
+template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16>
+__global__ __launch_bounds__((PassCfg<R, C, VPT>::NT),
+                             (MODE == 3 && LP >= 4 && PassCfg<R, C, VPT>::waves_per_eu > 2
                                   ? 2
-                                  : PassCfg<R, C, vpt_of<T>()>::waves_per_eu))
+                                  : PassCfg<R, C, VPT>::waves_per_eu))
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
-    cx<T> v[PassShape<R, vpt_of<T>()>::Q];
+    cx<T> v[PassShape<R, VPT>::Q];
     // one tile per workgroup: a persistent tile loop (1, 2 or 4 resident
     // workgroups per CU walking the tiles) measured 1.4-1.7x slower at 2^28
     // fp64
-    pass_stages<T, R, C, MODE, NTS, LP, 0>(a, reinterpret_cast<T*>(pifft_smem), v, (int)threadIdx.x,
+    pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, reinterpret_cast<T*>(pifft_smem), v, (int)threadIdx.x,
                                            tile_of_block(blockIdx.x, a.log_xg, gridDim.x));
 }
 

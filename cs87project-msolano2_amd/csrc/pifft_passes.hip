@@ -11,11 +11,12 @@
 
 using namespace pifft;
 
-#define PK(T, PREC, R, C, MODE, NTS, LP)                                                               \
-    PassKernel {                                                                                       \
-        PREC, R, C, MODE, NTS, LP, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS, LP>), \
-            PassCfg<R, C, vpt_of<T>()>::NT, PassCfg<R, C, vpt_of<T>()>::lds_elems * (int)sizeof(T)                              \
+#define PKV(T, PREC, R, C, MODE, NTS, LP, VPT)                                                          \
+    PassKernel {                                                                                         \
+        PREC, R, C, MODE, NTS, LP, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS, LP, VPT>), \
+            PassCfg<R, C, VPT>::NT, pass_lds_bytes<T, R, C, MODE, VPT>(), VPT                          \
     }
+#define PK(T, PREC, R, C, MODE, NTS, LP) PKV(T, PREC, R, C, MODE, NTS, LP, 16)
 
 namespace {
 const PassKernel kTable[] = {

@@ -9,6 +9,7 @@ struct PassKernel {
     const void* fn;
     int nt;
     int lds_bytes;
+    int vpt;  // values per thread (16, or 8 for small single-pass launches)
 };
 
 }  // namespace pifft

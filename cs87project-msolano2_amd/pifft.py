@@ -51,6 +51,7 @@ class PlanInfo(ctypes.Structure):
         ("launch_bytes", ctypes.c_uint64 * MAX_LAUNCH_INFO),
         ("launch_kind", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("launch_fn", ctypes.c_int32 * MAX_LAUNCH_INFO),
+        ("vpt", ctypes.c_int32 * 8),
     ]
 
 
@@ -229,6 +230,7 @@ def describe_info(i: PlanInfo) -> dict:
         "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, MAX_LAUNCH_INFO)]],
         "chunk_pairs": i.chunk_pairs,
         "launch_fn": list(i.launch_fn[: min(nl, MAX_LAUNCH_INFO)]),
+        "vpt": list(i.vpt[: i.num_passes]),
     }
 
 

@@ -84,6 +84,8 @@ typedef struct pifft_plan_info {
     int32_t launch_fn[PIFFT_MAX_LAUNCH_INFO]; /* kernel of each launch: launches with the same id
                                   run the same kernel function (ids 0, 1, ... in order
                                   of first use) -- what rocprof aggregates per kernel */
+    int32_t vpt[8];          /* complex values per thread of each pass (16; 8 for single
+                                passes too small to fill the GPU at 16)            */
 } pifft_plan_info;
 
 /* Last error message of the calling thread ("" if none). */
