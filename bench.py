@@ -312,15 +312,16 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
     return out
 
 
-def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev) -> dict:
+def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev, log_n=32) -> dict:
     """Config 5 on a multi-GPU job: fp64 N=2^32 split over `world` GPUs (one
     worker per GPU, 64 GiB input replica each), then the RCCL all-gather and
-    interleave into natural order (timed separately)."""
+    interleave into natural order (timed separately).  log_n < 32: a smaller
+    rehearsal of the same code path."""
     import pifft_dist
-    log_n = 32
     n = 1 << log_n
-    rec = {"workload": f"config 5: fp64 N=2^32 over {world} GPUs, one worker each (no data-path collective), "
-                       f"then the RCCL all-gather + interleave"}
+    rec = {"workload": f"config 5: fp64 N=2^{log_n} over {world} GPUs, one worker each (no data-path collective), "
+                       f"then the all-gather ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()}) "
+                       f"+ interleave"}
     job = Job(pifft, torch, gpu, n=n, P=world, prec=pifft.F64, first=rank, count=1, batch_local=1, b_first=0,
               seed=seed)
     elapsed = pifft_dist.max_over_ranks(job.run(steps, warmup, barrier), red_dev)
@@ -371,6 +372,8 @@ def main() -> int:
     ap.add_argument("--no-allgather", dest="allgather", action="store_false")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip configs 1-3 (at 1 GPU) / config 5 (at 8 GPUs) beside the headline step")
+    ap.add_argument("--c5-log-n", type=int, default=32,
+                    help="config 5 size at 8 GPUs (default 2^32; smaller only to rehearse the code path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-log-n", type=int, default=0, help="CPU baseline size (default: the headline N)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -467,10 +470,10 @@ def main() -> int:
         if world == 1 and args.log_n == 28 and args.prec == 64 and args.batch == 1:
             secondary = secondary_configs(pifft, torch, gpu, args.steps, args.warmup, args.seed, args.cpu_threads,
                                           not args.no_cpu_baseline)
-        elif world == 8 and args.shard == "workers" and not args.same_device:
+        elif world == 8 and args.shard == "workers" and (not args.same_device or args.c5_log_n < 32):
             try:
                 secondary = {"C5": config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
-                                           min(args.warmup, 2), args.seed, barrier, red_dev)}
+                                           min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n)}
             except Exception as e:  # reported, never silently replaced
                 secondary = {"C5": {"error": repr(e)}}
 

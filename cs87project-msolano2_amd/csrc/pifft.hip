@@ -279,11 +279,15 @@ int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines,
     return C;
 }
 
-// non-temporal streaming when a pass moves more than the Infinity Cache holds
+// non-temporal streaming when a pass moves more than the Infinity Cache holds,
+// and for 16-64 MiB passes (measured on MI355X, profiles/r02_nt_sweep.log:
+// fp64 2^20 P=1 26 -> 24 us, P=8 44 -> 41 us, fp32 4096 x 1024 16 -> 13 us,
+// the 2^21-point worker of 8 95 -> 84 us; but 8-16 MiB and 128-256 MiB passes
+// lose 5-40 %)
 int pick_nts(uint64_t pass_bytes) {
     const int force = env_int("PIFFT_NT", -1);
     if (force >= 0) return force ? 1 : 0;
-    return pass_bytes > (256ull << 20) ? 1 : 0;
+    return (pass_bytes > (256ull << 20) || (pass_bytes > (16ull << 20) && pass_bytes <= (64ull << 20))) ? 1 : 0;
 }
 
 // HBM rate of a pass side, by the contiguous bytes per row segment (TB/s).

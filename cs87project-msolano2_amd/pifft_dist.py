@@ -60,12 +60,20 @@ def slice_of_natural(X: np.ndarray, P: int, q: int) -> np.ndarray:
 
 
 def allgather_slices(local, group=None):
-    """All-gather equal-size per-rank slice tensors (rank order)."""
+    """All-gather equal-size per-rank slice tensors (rank order) into one
+    tensor.  RCCL: a single all_gather_into_tensor straight into the gathered
+    buffer (no per-rank parts and no concatenation copy: at config 5 that is
+    64 GiB per GPU saved), complex values moved as their real view."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     src = local.contiguous()
-    staged = dist.get_backend(group) == "gloo" and src.is_cuda  # gloo gathers host tensors
+    if dist.get_backend(group) == "nccl":
+        flat = torch.view_as_real(src).reshape(-1) if src.is_complex() else src.reshape(-1)
+        out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
+        dist.all_gather_into_tensor(out, flat, group=group)
+        return torch.view_as_complex(out.view(-1, 2)) if src.is_complex() else out
+    staged = src.is_cuda  # gloo gathers host tensors
     if staged:
         src = src.cpu()
     parts = [torch.empty_like(src) for _ in range(world)]
