@@ -263,9 +263,18 @@ int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines,
     int C = env_int(env_c, 0);
     // single pass: lines are whole contiguous transforms, no segment-width
     // constraint -> small tiles (measured best: C = 4096/R, i.e. C=1 at 4096)
-    const int tile = mode == 0   ? env_int(prec == 64 ? "PIFFT_SINGLE_TILE64" : "PIFFT_SINGLE_TILE32", 4096)
-                     : mode == 1 ? env_int(prec == 64 ? "PIFFT_FIRST_TILE64" : "PIFFT_FIRST_TILE32", tile_elems(prec))
-                                 : tile_elems(prec);
+    int tile = mode == 0   ? env_int(prec == 64 ? "PIFFT_SINGLE_TILE64" : "PIFFT_SINGLE_TILE32", 4096)
+               : mode == 1 ? env_int(prec == 64 ? "PIFFT_FIRST_TILE64" : "PIFFT_FIRST_TILE32", tile_elems(prec))
+                           : tile_elems(prec);
+    // fp64 strided passes of R <= 256, not the fused tree pass (mode 3): a
+    // 4096-value tile.  At 8192 (R = 256, C = 32, 512 threads) the kernel
+    // spills 20 B/lane at its 128-VGPR budget; at C = 16 it runs 256 threads
+    // at 138 VGPRs, 3 workgroups per CU.  Measured on MI355X
+    // (profiles/r02_smallr_tile.log): 2^22 -7 %, 2^23 -12 %, 2^24 -4 %, the
+    // 2^28 worker of 8 -1.5 %; the fused pass itself loses at C = 16 (156
+    // VGPRs), so it keeps the 8192 tile
+    if (prec == 64 && (mode == 1 || mode == 2) && R <= 256) tile = env_int("PIFFT_SMALLR_TILE64", 4096);
+    if (mode == 3) mode = 1;  // the fused first pass: the first-pass tile, mode-1 line rules
     if (C <= 0) C = tile / R;
     if (C < 1) C = 1;
     if (C > 64) C = 64;
@@ -346,7 +355,8 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             for (size_t p = 0; p < logs.size(); p++) {
                 const int R = 1 << logs[p], mode = p == 0 ? 1 : 2;
                 const int C = pick_lines(prec, R, M >> logs[p], ntrans * (M >> logs[p]),
-                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
+                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32",
+                                         (p == 0 && heavy_lp) ? 3 : mode);
                 if (!find_pass(prec, R, C, mode, nts)) return fail("no pass kernel R=%d C=%d", R, C);
                 out.push_back({R, C, mode, nts});
             }
@@ -378,7 +388,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             if (force_order < 0 && heavy_lp > 0 && order == 1) {
                 const int R0 = 1 << (base + (extra > 0 ? 1 : 0));
                 const int C0 = pick_lines(prec, R0, M >> ilog2u((uint64_t)R0), ntrans * (M >> ilog2u((uint64_t)R0)),
-                                          prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", 1);
+                                          prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", 3);
                 if (prec != 64 || (size_t)C0 * esz >= 256) continue;  // fp32: measured cases only
             }
             std::vector<PassChoice> cand;
@@ -389,7 +399,8 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
                 const int R = 1 << bits;
                 const int mode = p == 0 ? 1 : 2;
                 const int C = pick_lines(prec, R, M >> bits, ntrans * (M >> bits),
-                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", mode);
+                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32",
+                                         (p == 0 && heavy_lp) ? 3 : mode);
                 if (!find_pass(prec, R, C, mode, nts)) { ok = false; break; }
                 const double rs = seg_rate((double)C * esz);           // strided side
                 const double side = (double)ntrans * M * esz * 1e-12;  // TB per side
