@@ -22,3 +22,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/stats_c4" -o c4 -- \
 rocpd2summary -i "$out/stats_c4/c4_results.db" -f csv -d "$out/sum_c4" -o c4 > /dev/null 2>&1 || exit 1
 grep '^{' "$out/stats_c4.log" > "$out/${tag}_bench_under_rocprof.json" || true
 cat "$out/sum_c4/"*.csv | head -8
+python3 tools/rocpd_timed_avg.py "$out/stats_c4/c4_results.db" 10 "$out/${tag}_kernel_timed_avg.csv" || exit 1
+cat "$out/${tag}_kernel_timed_avg.csv"
