@@ -595,8 +595,37 @@ __device__ __forceinline__ void pl_swap(cx<T>& a, cx<T>& b) {
     __builtin_memcpy(&b, y, sizeof b);
 }
 
+// Stage twiddles fetched with the data (PIFFT_TW_PREFETCH): the base anchor
+// w of every later stage's butterflies is loaded right after the tile's
+// inputs are issued, and w^2, w^4, w^8 are formed by squaring when the stage
+// runs -- instead of 2-4 table loads at the start of each stage, each a
+// dependent round trip on a workgroup's critical path.  That path is what
+// bounds the latency-bound small launches (one or two workgroups per CU);
+// the streaming passes hide it behind the other workgroup.
+// 0: off; 1: single passes (MODE 0/4) only; 2: every pass.  Measured on
+// MI355X (profiles/r02_ab_twiddle_prefetch.log): no gain on the small
+// launches (fp32 4096 x 512: 9 us either way; fp64 2^20: 24 us either way),
+// fp64 8192 x 64 single passes 11 -> 15 us (registers), C4 +3 % at 2 -- so off.
+#ifndef PIFFT_TW_PREFETCH
+#define PIFFT_TW_PREFETCH 0
+#endif
+template <int R, int C, int BM, int VPT>
+constexpr bool tw_prefetch() {
+    return PIFFT_TW_PREFETCH == 2 || (PIFFT_TW_PREFETCH == 1 && BM == 0);
+}
+// anchors of stages 1 .. S-1 (one per butterfly of a thread)
+template <int R, int C, int BM, int VPT, int S>
+constexpr int pre_offset() {
+    if constexpr (S <= 1) return 0;
+    else return pre_offset<R, C, BM, VPT, S - 1>() + Stage<R, C, BM, S - 1, VPT>::U;
+}
+template <int R, int C, int BM, int VPT>
+constexpr int pre_count() {
+    return pre_offset<R, C, BM, VPT, PassShape<R, VPT>::NSTG>();
+}
+
 template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT>
-__device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
+__device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, cx<T>* pre, int tid, uint64_t tile) {
     using C2 = cx<T>;
     // MODE | 4: the same pass storing at bitrev_{log2 M}(natural position),
     // the reference's scratch order (PIFFT_OUT_BITREV; last pass only).  Each
@@ -688,6 +717,19 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             }
         }
     }
+    if constexpr (St::first && tw_prefetch<R, C, BM, VPT>()) {
+        const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
+        static_for<1, Sh::NSTG, 1>([&](auto sc) {
+            constexpr int S2 = decltype(sc)::value;
+            using St2 = Stage<R, C, BM, S2, VPT>;
+#pragma unroll
+            for (int u = 0; u < St2::U; u++) {
+                int c, b;
+                St2::map(tid, u, c, b);
+                pre[pre_offset<R, C, BM, VPT, S2>() + u] = twr[(b & (St2::ns - 1)) * (R / (St2::ns * St2::q))];
+            }
+        });
+    }
     // ---- twiddles before the butterflies ----
     if constexpr (St::first && BM == 2) {
         // w_{Ns R}^{(j mod Ns) r}, r = b + k NB: the k-dependent factor
@@ -710,8 +752,14 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const int e1 = (b & (ns - 1)) * (R / (ns * q));
             C2 anc[4];
+            if constexpr (tw_prefetch<R, C, BM, VPT>()) {
+                anc[0] = pre[pre_offset<R, C, BM, VPT, S>() + u];
 #pragma unroll
-            for (int i = 0; (1 << i) < q; i++) anc[i] = twr[e1 << i];
+                for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
+            } else {
+#pragma unroll
+                for (int i = 0; (1 << i) < q; i++) anc[i] = twr[e1 << i];
+            }
             apply_powers<q>(&v[u * q], anc);
         }
     }
@@ -771,7 +819,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #pragma unroll
             for (int g = 0; g < 8; g++) pl_swap<16>(v[2 * g], v[2 * g + 1]);
         }
-        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
         using Nx = Stage<R, C, BM, S + 1, VPT>;
@@ -799,7 +847,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 }
             }
         }
-        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile);
     }
 }
 
@@ -818,10 +866,11 @@ __global__ __launch_bounds__((PassCfg<R, C, VPT>::NT),
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     cx<T> v[PassShape<R, VPT>::Q];
+    cx<T> pre[pre_count<R, C, MODE & 3, VPT>() > 0 ? pre_count<R, C, MODE & 3, VPT>() : 1];
     // one tile per workgroup: a persistent tile loop (1, 2 or 4 resident
     // workgroups per CU walking the tiles) measured 1.4-1.7x slower at 2^28
     // fp64
-    pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, reinterpret_cast<T*>(pifft_smem), v, (int)threadIdx.x,
+    pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, reinterpret_cast<T*>(pifft_smem), v, pre, (int)threadIdx.x,
                                            tile_of_block(blockIdx.x, a.log_xg, gridDim.x));
 }
 

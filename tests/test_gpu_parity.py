@@ -136,6 +136,28 @@ def test_tree_stage_bitwise_every_worker(suf, logn, P):
 
 
 @pytest.mark.parametrize("suf", list(DT))
+@pytest.mark.parametrize("logn,P", [(20, 512), (18, 4096)])
+def test_multi_launch_tree_in_place_large_p(suf, logn, P):
+    """log2 P > 4: the tree runs as ceil(log2 P / 4) launches, all but the
+    first in place over the plan's tree buffer (k_tree without __restrict__).
+    A sample of workers, bit for bit against the oracle's post-tree segments,
+    and the whole transform against the oracle."""
+    n = 1 << logn
+    m = n // P
+    x = oracle.generate(n, DT[suf], seed=P)
+    d_in = dev(x)
+    plan = pifft.Plan(n, P, 1, PREC[suf], first=0, count=P, device=0, flags=pifft.OUT_SLICES)
+    assert plan.describe()["tree_launches"] == (P.bit_length() - 1 + 3) // 4
+    d_all = torch.empty(n, dtype=d_in.dtype, device="cuda")
+    plan.tree_device(d_in.data_ptr(), d_all.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = d_all.cpu().numpy()
+    for q in sorted({0, 1, P // 3, P // 2 + 1, P - 2, P - 1}):
+        assert got[q * m:(q + 1) * m].tobytes() == oracle.tree_segment(x, P, q).tobytes(), f"q={q}"
+    assert_bins_close(run(pifft.Plan(n, P, 1, PREC[suf]), x), oracle.fft(x, P=1, nthreads=8), suf, n)
+
+
+@pytest.mark.parametrize("suf", list(DT))
 def test_generator_bitwise(suf):
     n = 1 << 16
     d = torch.empty(n, dtype=TDT[DT[suf]], device="cuda")
