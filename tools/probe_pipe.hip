@@ -42,9 +42,15 @@ __device__ __forceinline__ void addr(const Map& m, uint64_t tile, int g, uint64_
     } else if (m.pass == 4) {  // two-pass 2^14 x 2^14, first pass: 16-B column gather, contiguous write
         src = j + ((uint64_t)r << 14);
         dst = (j << 14) + r;
-    } else {  // two-pass, second pass: 16-B gather and 16-B scatter
+    } else if (m.pass == 5) {  // two-pass, second pass: 16-B gather and 16-B scatter
         src = j + ((uint64_t)r << 14);
         dst = src;
+    } else if (m.pass == 6) {  // "W" order, pass 1: as p1 in, out (n3, n2, k1): 16-KiB runs 8 MiB apart
+        src = j + ((uint64_t)r << 18);
+        dst = ((j & 511) << 19) + ((j >> 9) << 10) + r;
+    } else {  // "W" order, passes 2 and 3: windowed read (rows 16 KiB apart), spread write (rows 8 MiB apart)
+        src = ((j >> 10) << 19) + ((uint64_t)r << 10) + (j & 1023);
+        dst = j + ((uint64_t)r << 19);
     }
     src = padded(src, m.src_s, m.src_p);
     dst = padded(dst, m.dst_s, m.dst_p);
@@ -163,26 +169,21 @@ int main() {
     // 2^14: one 16384-value column per workgroup (1024 threads), 16-B accesses
     // on the column side; 8 (or 2^xg) adjacent columns on one XCD share lines
     // through its L2.  Against the three-pass copies of the same box.
-    const Map maps[] = {{10, 3, 1, 0, 0, 0, 0}, {9, 4, 2, 0, 0, 0, 0}, {9, 4, 3, 0, 0, 0, 0}};
-    const Map two[] = {{14, 0, 4, 0, 0, 0, 0}, {14, 0, 5, 0, 0, 0, 0}};
-    for (int round = 0; round < 2; round++) {
-        uint32_t xg = 2;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_log_xg), &xg, 4);
-        for (const Map& m : maps) {
+    // The C4 passes in the k_pass order (A: p1, p2, p3) against an alternative
+    // choice of the two intermediate layouts ("W": p6, then p7 twice), 4
+    // rounds interleaved on one box
+    const Map maps[] = {{10, 3, 1, 0, 0, 0, 0}, {9, 4, 2, 0, 0, 0, 0}, {9, 4, 3, 0, 0, 0, 0},
+                        {10, 3, 6, 0, 0, 0, 0}, {9, 4, 7, 0, 0, 0, 0}};
+    for (int round = 0; round < 4; round++) {
+        float t[5];
+        for (int i = 0; i < 5; i++) {
+            const Map& m = maps[i];
             const uint32_t ntiles = (uint32_t)(n >> (m.log_r + m.log_c));
-            const float t_once = time([&] { hipLaunchKernelGGL(k_once<512>, dim3(ntiles), dim3(512), 72 * 1024, 0, x, y, m); });
-            printf("round %d pass %d R=%d C=%d: %.3f ms %.0f GB/s\n", round, m.pass, 1 << m.log_r, 1 << m.log_c, t_once,
-                   2.0 * n * 16 / t_once / 1e6);
+            t[i] = time([&] { hipLaunchKernelGGL(k_once<512>, dim3(ntiles), dim3(512), 72 * 1024, 0, x, y, m); });
+            printf("round %d pass %d R=%d C=%d: %.3f ms %.0f GB/s\n", round, m.pass, 1 << m.log_r, 1 << m.log_c, t[i],
+                   2.0 * n * 16 / t[i] / 1e6);
         }
-        for (uint32_t xgv : {0u, 2u, 3u, 4u}) {
-            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_log_xg), &xgv, 4);
-            for (const Map& m : two) {
-                const uint32_t ntiles = (uint32_t)(n >> (m.log_r + m.log_c));
-                const float t = time([&] { hipLaunchKernelGGL(k_once<1024>, dim3(ntiles), dim3(1024), 140 * 1024, 0, x, y, m); });
-                printf("round %d two-pass %s (xcd group 2^%u): %.3f ms %.0f GB/s\n", round,
-                       m.pass == 4 ? "A: gather -> contiguous" : "B: gather -> scatter", xgv, t, 2.0 * n * 16 / t / 1e6);
-            }
-        }
+        printf("round %d  A total %.3f ms   W total %.3f ms\n", round, t[0] + t[1] + t[2], t[3] + 2 * t[4]);
         fflush(stdout);
     }
     if (hipGetLastError() != hipSuccess) return 2;
