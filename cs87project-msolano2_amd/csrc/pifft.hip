@@ -245,6 +245,22 @@ TwoLevel two_level(TableBuilder& tb, uint64_t L) {
     return t;
 }
 
+// slice-major -> natural order: k_interleave_tile (LDS tile of all P slices,
+// P <= 2048) from P = 2^5 at fp64 and P = 2 at fp32, else k_interleave (one
+// thread per output element, any P); profiles/r02_interleave_ab.log
+bool interleave_tiled(int prec, int lp, uint64_t n) {
+    const int lo = env_int(prec == 64 ? "PIFFT_INTERLEAVE_TILE_MIN64" : "PIFFT_INTERLEAVE_TILE_MIN32", prec == 64 ? 5 : 1);
+    return lo > 0 && lp >= lo && lp <= 11 && n >= (uint64_t)IL_TILE;
+}
+const void* interleave_fn(int prec, int lp, uint64_t n) {
+    if (interleave_tiled(prec, lp, n))
+        return prec == 64 ? (const void*)&k_interleave_tile<double> : (const void*)&k_interleave_tile<float>;
+    return prec == 64 ? (const void*)&k_interleave<double> : (const void*)&k_interleave<float>;
+}
+uint64_t interleave_threads(uint64_t total, int lp, int prec, uint64_t n) {
+    return interleave_tiled(prec, lp, n) ? (total / IL_TILE) * 256 : total;
+}
+
 struct PassChoice {
     int R, C, mode, nts;
     int vpt = 16;
@@ -715,12 +731,12 @@ int build_plan(pifft_plan* p, bool dry = false) {
     if (p->natural && p->P > 1) {
         Step s;
         s.kind = STEP_INTERLEAVE;
-        s.fn = p->prec == 64 ? (const void*)&k_interleave<double> : (const void*)&k_interleave<float>;
+        s.fn = interleave_fn(p->prec, p->lp, p->n);
         s.il_total = (uint64_t)p->batch * p->n;
         s.il_log_n = (uint32_t)p->log_n;
         s.il_log_p = (uint32_t)p->lp;
         s.block = dim3(256);
-        s.grid = dim3(stride_grid(s.il_total));
+        s.grid = dim3(stride_grid(interleave_threads(s.il_total, p->lp, p->prec, p->n)));
         s.bytes = 2 * s.il_total * esz;
         Elem e;
         e.steps.push_back(s);
@@ -916,18 +932,15 @@ int ensure_host_staging(pifft_plan* p) {
 
 int launch_interleave(const void* d_slices, void* d_out, uint64_t n, uint32_t workers, uint32_t batch, int prec,
                       hipStream_t st) {
-    const uint64_t total = (uint64_t)batch * n;
-    const dim3 blk(256), grd(stride_grid(total));
-    const uint32_t ln = (uint32_t)ilog2u(n), lpp = (uint32_t)ilog2u(workers);
-    if (prec == PIFFT_F64)
-        hipLaunchKernelGGL(k_interleave<double>, grd, blk, 0, st, (const cx<double>*)d_slices, (cx<double>*)d_out,
-                           total, ln, lpp);
-    else if (prec == PIFFT_F32)
-        hipLaunchKernelGGL(k_interleave<float>, grd, blk, 0, st, (const cx<float>*)d_slices, (cx<float>*)d_out,
-                           total, ln, lpp);
-    else
-        return fail("bad precision");
-    HIPCHK(hipGetLastError());
+    if (prec != PIFFT_F64 && prec != PIFFT_F32) return fail("bad precision");
+    uint64_t total = (uint64_t)batch * n;
+    const int lp = ilog2u(workers);
+    uint32_t ln = (uint32_t)ilog2u(n), lpp = (uint32_t)lp;
+    const void* in = d_slices;
+    void* o = d_out;
+    void* args[] = {&in, &o, &total, &ln, &lpp};
+    HIPCHK(hipLaunchKernel(interleave_fn(prec, lp, n), dim3(stride_grid(interleave_threads(total, lp, prec, n))),
+                           dim3(256), args, 0, st));
     return 0;
 }
 

@@ -193,6 +193,40 @@ __device__ __forceinline__ cx<T> tw2(const cx<T>* __restrict__ lo, const cx<T>* 
     return cmul(b, a);
 }
 
+// w_NS^e = (cos 2 pi e/NS, -sin 2 pi e/NS), e < NS, evaluated at compile time
+// (Taylor series on the first quadrant, then the quadrant's exact rotation)
+template <int NS>
+struct RootsOf {
+    double re[NS], im[NS];
+    constexpr RootsOf() : re(), im() {
+        constexpr double two_pi = 6.283185307179586476925286766559;
+        for (int e = 0; e < NS; e++) {
+            const int quad = (4 * e) / NS, r = e - quad * (NS / 4);
+            const double x = two_pi * r / NS;  // [0, pi/2)
+            double c = 1, s = x, tc = 1, ts = x;
+            for (int i = 1; i < 16; i++) {
+                tc *= -x * x / ((2 * i - 1) * (2 * i));
+                ts *= -x * x / ((2 * i) * (2 * i + 1));
+                c += tc;
+                s += ts;
+            }
+            const double cq = quad == 0 ? c : quad == 1 ? -s : quad == 2 ? -c : s;
+            const double sq = quad == 0 ? s : quad == 1 ? c : quad == 2 ? -s : -c;
+            re[e] = cq;
+            im[e] = -sq;
+        }
+    }
+};
+
+// for (I = B; I < E; I += S) f(integral_constant<I>) -- compile-time indices
+template <int B, int E, int S, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + S, E, S>(f);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Tree ("funnel") network, shared by k_tree and the fused first pass
 // ---------------------------------------------------------------------------
@@ -216,10 +250,45 @@ __device__ __forceinline__ cx<T> tree_tw(const TreeTw& tw, uint64_t e) {
 // only branches leading to workers [q0, q1) are evaluated (uniform branches,
 // compile-time register indices).  Operation order = butterfly_left /
 // butterfly_right (CPU.c:540-576): add, or (sub) * omega.
+// With the reference-formula table (tw.direct, N <= 2^22) every twiddle is a
+// table entry, so the output is bit-identical to the reference.  With the
+// two-level table the twiddle of position i + ml D at level t factors as
+// w_N^{i 2^t} * w_{2^(L-tl)}^{ml} (D 2^t / N = 2^(tl-L)): one table lookup
+// per level and thread, times a compile-time root (the fused pass's
+// tree_path_steps does the same), instead of one two-level lookup per
+// butterfly.
 template <typename T, int L>
 __device__ __forceinline__ void tree_levels(cx<T>* v, const TreeTw& tw, uint64_t i, uint32_t log_d, uint32_t t0,
                                             uint64_t blk0, uint32_t log_w, uint64_t q0, uint64_t q1) {
     constexpr int V = 1 << L;
+    if (!tw.direct) {
+        cx<T> base[L];
+#pragma unroll
+        for (int tl = 0; tl < L; tl++) base[tl] = tree_tw<T>(tw, i << (t0 + tl));
+        static_for<0, L, 1>([&](auto tlc) {
+            constexpr int tl = decltype(tlc)::value;
+            constexpr int BS = V >> tl, H = BS >> 1, NS = 1 << (L - tl);
+            constexpr RootsOf<NS> roots{};
+#pragma unroll
+            for (int blk = 0; blk < (1 << tl); blk++) {
+                const int lo = blk * BS;
+                const uint64_t cl0 = (((blk0 << L) + lo) << log_w), cl1 = (((blk0 << L) + lo + H) << log_w);
+                const uint64_t cr1 = (((blk0 << L) + lo + BS) << log_w);
+                const bool needL = (cl0 < q1) && (cl1 > q0);
+                const bool needR = (cl1 < q1) && (cr1 > q0);
+#pragma unroll
+                for (int ml = 0; ml < H; ml++) {
+                    const cx<T> x0 = v[lo + ml], x1 = v[lo + ml + H];
+                    if (needL) v[lo + ml] = cadd(x0, x1);
+                    if (needR) {
+                        const cx<T> s{(T)roots.re[ml], (T)roots.im[ml]};
+                        v[lo + ml + H] = cmul(csub(x0, x1), ml ? cmul(base[tl], s) : base[tl]);
+                    }
+                }
+            }
+        });
+        return;
+    }
 #pragma unroll
     for (int tl = 0; tl < L; tl++) {
         const int BS = V >> tl, H = BS >> 1;
@@ -267,31 +336,6 @@ __device__ __forceinline__ cx<T> tree_path(cx<T>* v, const TreeTw& tw, uint64_t 
     return v[0];
 }
 
-// w_NS^e = (cos 2 pi e/NS, -sin 2 pi e/NS), e < NS, evaluated at compile time
-// (Taylor series on the first quadrant, then the quadrant's exact rotation)
-template <int NS>
-struct RootsOf {
-    double re[NS], im[NS];
-    constexpr RootsOf() : re(), im() {
-        constexpr double two_pi = 6.283185307179586476925286766559;
-        for (int e = 0; e < NS; e++) {
-            const int quad = (4 * e) / NS, r = e - quad * (NS / 4);
-            const double x = two_pi * r / NS;  // [0, pi/2)
-            double c = 1, s = x, tc = 1, ts = x;
-            for (int i = 1; i < 16; i++) {
-                tc *= -x * x / ((2 * i - 1) * (2 * i));
-                ts *= -x * x / ((2 * i) * (2 * i + 1));
-                c += tc;
-                s += ts;
-            }
-            const double cq = quad == 0 ? c : quad == 1 ? -s : quad == 2 ? -c : s;
-            const double sq = quad == 0 ? s : quad == 1 ? c : quad == 2 ? -s : -c;
-            re[e] = cq;
-            im[e] = -sq;
-        }
-    }
-};
-
 // tree_path for a thread's k-th first-pass input z_q[zi], zi = zi0 + k M/Q
 // (the fused first pass): its level-t twiddle w_N^{(zi + ml M) 2^t} is
 // bt[t] = w_N^{zi0 2^t} times the compile-time constant w_{QP}^{(k + Q ml) 2^t}
@@ -317,15 +361,6 @@ __device__ __forceinline__ cx<T> tree_path_steps(cx<T>* v, const cx<T>* bt, uint
         }
     }
     return v[0];
-}
-
-// for (I = B; I < E; I += S) f(integral_constant<I>) -- compile-time indices
-template <int B, int E, int S, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + S, E, S>(f);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -945,6 +980,47 @@ __global__ __launch_bounds__(256) void k_interleave(const cx<T>* __restrict__ in
         const uint32_t rr = (uint32_t)(o & ((1ull << log_p) - 1));
         const uint32_t q = log_p ? (__builtin_bitreverse32(rr) >> (32 - log_p)) : 0u;
         out[gid] = in[bt * n + ((uint64_t)q << (log_n - log_p)) + k];
+    }
+}
+
+// The same through an LDS tile of all P slices x K = 2048/P consecutive k
+// (P <= 2048): every slice is read in runs of K elements (>= 256 B for
+// P <= 128 at fp64) and the tile's 2048 outputs out[P k + r] are one
+// contiguous block -- instead of P different rows per wave instruction
+// (k_interleave: 16-B pieces for P >= 64).  Measured on MI355X
+// (profiles/r02_interleave_ab.log): fp64 2^28 P = 64 4.05 -> 1.55 ms, 2^24
+// P = 256 0.34 -> 0.09 ms, fp32 2^24 P = 8 0.053 -> 0.044 ms; for fp64 P <= 16
+// k_interleave is as fast or faster (2^28 P = 8: 1.52 vs 1.62 ms).
+constexpr int IL_TILE = 2048;
+template <typename T>
+__global__ __launch_bounds__(256) void k_interleave_tile(const cx<T>* __restrict__ in, cx<T>* __restrict__ out,
+                                                         uint64_t total, uint32_t log_n, uint32_t log_p) {
+    __shared__ cx<T> tile[IL_TILE + IL_TILE / 16];
+    const uint32_t log_k = 11 - log_p;  // K = 2048 / P
+    const uint32_t log_m = log_n - log_p;
+    const uint64_t ntiles = total >> 11;
+    const uint32_t P = 1u << log_p;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t e0 = t << 11;  // first output of the tile
+        const uint64_t bt = e0 >> log_n, k0 = (e0 & ((1ull << log_n) - 1)) >> log_p;
+        const cx<T>* src = in + (bt << log_n) + k0;
+        __syncthreads();  // the previous tile's reads are done
+#pragma unroll
+        for (int i = 0; i < IL_TILE / 256; i++) {
+            const uint32_t e = threadIdx.x + i * 256;
+            const uint32_t q = e >> log_k, k = e & ((1u << log_k) - 1);
+            const uint32_t r = log_p ? (__builtin_bitreverse32(q) >> (32 - log_p)) : 0u;
+            const uint32_t o = (k << log_p) + r;  // natural position within the tile
+            tile[o + (o >> 4)] = src[((uint64_t)q << log_m) + k];
+        }
+        __syncthreads();
+        cx<T>* dst = out + e0;
+#pragma unroll
+        for (int i = 0; i < IL_TILE / 256; i++) {
+            const uint32_t o = threadIdx.x + i * 256;
+            dst[o] = tile[o + (o >> 4)];
+        }
+        (void)P;
     }
 }
 
