@@ -159,3 +159,66 @@ def test_config5_all_workers_n2e32():
     assert nat_bins.tobytes() == got.tobytes()
     nn2 = torch.linalg.vector_norm(natural).item() ** 2
     assert nn2 == pytest.approx(un2, rel=1e-13)
+
+
+@pytest.mark.timeout(600)
+def test_config4_fp32_full_size_vs_oracle():
+    """The reference's own precision (data_t = float, CPU.c:33-36) at N = 2^28:
+    the 4-pass 128^4 fp32 plan and the 8-worker plan against the oracle (fp32
+    restatement, 16 workers).  Bar: rel-L2 <= 1e-5 log2 N."""
+    n, logn = 1 << 28, 28
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F32, stream=st)
+    got = {}
+    for P in (1, 8):
+        plan = pifft.Plan(n, P, 1, pifft.F32)
+        y = torch.empty_like(x)
+        plan.execute_device(x.data_ptr(), y.data_ptr(), st)
+        torch.cuda.synchronize()
+        got[P] = y.cpu().numpy()
+        plan.close()
+        del y
+    xh = x.cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
+    want = oracle.fft(xh, P=16, nthreads=_threads())
+    for P, g in got.items():
+        _check_bins(g, want, tol=1e-5 * logn)
+
+
+@pytest.mark.timeout(600)
+def test_reference_max_size_n2e30_fp64():
+    """N = 2^30, the largest size the reference can express (uint32_t N and
+    atoi, CPU.c:41,139): the 1-worker and 8-worker plans agree bin for bin,
+    FFT(conj(FFT(x))) = N conj(x), Parseval, and 16 direct DFT bins."""
+    free, _ = torch.cuda.mem_get_info()
+    assert free >= 80 * (1 << 30), f"needs ~80 GiB of HBM, {free / 2**30:.0f} GiB free"
+    n = 1 << 30
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=st)
+    X = torch.empty_like(x)
+    p1 = pifft.Plan(n, 1, 1, pifft.F64)
+    p1.execute_device(x.data_ptr(), X.data_ptr(), st)
+    Y = torch.empty_like(x)
+    p8 = pifft.Plan(n, 8, 1, pifft.F64)
+    p8.execute_device(x.data_ptr(), Y.data_ptr(), st)
+    torch.cuda.synchronize()
+    p8.close()
+    err = (torch.linalg.vector_norm(Y - X) / torch.linalg.vector_norm(X)).item()
+    assert err <= TOL64, err
+    xn = torch.linalg.vector_norm(x).item()
+    assert abs(torch.linalg.vector_norm(X).item() ** 2 / n - xn ** 2) <= 1e-12 * xn ** 2
+    ks = [0, 1, 3, 12345, n // 2, n // 2 + 7, n - 1] + [int(k) for k in np.random.default_rng(30).integers(0, n, 9)]
+    want = _dft_bins_gemm(x, ks)
+    got = X[torch.as_tensor(ks, device="cuda")].cpu().numpy()
+    assert np.max(np.abs(got - want)) <= 1e-12 * xn * 50
+    # double transform
+    Xc = X.conj().resolve_conj()
+    del Y
+    Z = torch.empty_like(x)
+    p1.execute_device(Xc.data_ptr(), Z.data_ptr(), st)
+    torch.cuda.synchronize()
+    err2 = (torch.linalg.vector_norm(Z.conj() / n - x) / xn).item()
+    assert err2 <= TOL64, err2
