@@ -24,3 +24,8 @@ grep '^{' "$out/stats_c4.log" > "$out/${tag}_bench_under_rocprof.json" || true
 cat "$out/sum_c4/"*.csv | head -8
 python3 tools/rocpd_timed_avg.py "$out/stats_c4/c4_results.db" 10 "$out/${tag}_kernel_timed_avg.csv" || exit 1
 cat "$out/${tag}_kernel_timed_avg.csv"
+# the secondary configs' kernels (C1, C2, C2 slice, C3) under the same trace
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/stats_sec" -o sec -- \
+    python3 -u bench.py --no-cpu-baseline --steps 10 --warmup 3 > "$out/stats_sec.log" 2>&1 || exit 1
+rocpd2summary -i "$out/stats_sec/sec_results.db" -f csv -d "$out/sum_sec" -o sec > /dev/null 2>&1 || exit 1
+cat "$out/sum_sec/"*.csv | head -16
