@@ -160,8 +160,9 @@ def cpu_baseline(log_n: int, prec: int, threads: int, workers: int | None = None
 
 def load_traffic(config_key: str, launch_indices):
     """HBM bytes per launch of the dominant kernel (mean over its launches) from
-    the committed PMC summary (the newest profiles/*traffic*.json of this plan)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), key=os.path.getmtime)
+    the committed PMC summary (the last profiles/*traffic*.json of this plan by
+    name: round tags sort in order)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))  # r02_* after r01_*
     for f in reversed(files):
         try:
             d = json.load(open(f))

@@ -75,7 +75,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--outdir", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args, rest = ap.parse_known_args()
-    bench_args = ["--steps", str(args.steps), "--warmup", "1", "--no-cpu-baseline"] + rest
+    bench_args = ["--steps", str(args.steps), "--warmup", "1", "--no-cpu-baseline", "--no-secondary"] + rest
 
     ba = argparse.ArgumentParser()
     ba.add_argument("--prec", type=int, default=64)
