@@ -48,9 +48,21 @@ __device__ __forceinline__ void addr(const Map& m, uint64_t tile, int g, uint64_
     } else if (m.pass == 6) {  // "W" order, pass 1: as p1 in, out (n3, n2, k1): 16-KiB runs 8 MiB apart
         src = j + ((uint64_t)r << 18);
         dst = ((j & 511) << 19) + ((j >> 9) << 10) + r;
-    } else {  // "W" order, passes 2 and 3: windowed read (rows 16 KiB apart), spread write (rows 8 MiB apart)
+    } else if (m.pass == 7) {  // "W" order, passes 2 and 3: windowed read (rows 16 KiB apart), spread write (rows 8 MiB apart)
         src = ((j >> 10) << 19) + ((uint64_t)r << 10) + (j & 1023);
         dst = j + ((uint64_t)r << 19);
+    } else {
+        // the last pass of an all-8-worker plan at 2^28 (local 2^25 = 512 x 256
+        // x 256, last R = 256, Ns = 2^17): tile -> (worker q, line block),
+        // lines j < 2^17 of slice q read q 2^25 + j + r 2^17; written
+        // slice-major (pass 8) or straight to natural order bitrev(q) + 8 (j +
+        // r 2^17) (pass 9: 16-B pieces 128 B apart, the 8 workers' tiles of a
+        // line block consecutive, i.e. one XCD group)
+        const uint64_t q = tile & 7, jb = tile >> 3;
+        const uint64_t jj = jb * C + c;
+        const uint64_t rq = ((q & 1) << 2) | (q & 2) | ((q >> 2) & 1);
+        src = (q << 25) + jj + ((uint64_t)r << 17);
+        dst = m.pass == 8 ? src : rq + ((jj + ((uint64_t)r << 17)) << 3);
     }
     src = padded(src, m.src_s, m.src_p);
     dst = padded(dst, m.dst_s, m.dst_p);
@@ -81,6 +93,26 @@ __global__ __launch_bounds__(NT, 1024 / NT) void k_once(const d2* __restrict__ i
         uint64_t s, d;
         addr(m, tile, threadIdx.x + k * NT, s, d);
         __builtin_nontemporal_store(v[k], out + d);
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT, 1024 / NT) void k_once_plain(const d2* __restrict__ in, d2* __restrict__ out, Map m) {
+    extern __shared__ d2 dummy[];
+    const uint64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    d2 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        uint64_t s, d;
+        addr(m, tile, threadIdx.x + k * NT, s, d);
+        v[k] = __builtin_nontemporal_load(in + s);
+    }
+    if (threadIdx.x == 4095) dummy[0] = v[0];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        uint64_t s, d;
+        addr(m, tile, threadIdx.x + k * NT, s, d);
+        out[d] = v[k];
     }
 }
 
@@ -169,21 +201,23 @@ int main() {
     // 2^14: one 16384-value column per workgroup (1024 threads), 16-B accesses
     // on the column side; 8 (or 2^xg) adjacent columns on one XCD share lines
     // through its L2.  Against the three-pass copies of the same box.
-    // The C4 passes in the k_pass order (A: p1, p2, p3) against an alternative
-    // choice of the two intermediate layouts ("W": p6, then p7 twice), 4
-    // rounds interleaved on one box
-    const Map maps[] = {{10, 3, 1, 0, 0, 0, 0}, {9, 4, 2, 0, 0, 0, 0}, {9, 4, 3, 0, 0, 0, 0},
-                        {10, 3, 6, 0, 0, 0, 0}, {9, 4, 7, 0, 0, 0, 0}};
-    for (int round = 0; round < 4; round++) {
-        float t[5];
-        for (int i = 0; i < 5; i++) {
-            const Map& m = maps[i];
-            const uint32_t ntiles = (uint32_t)(n >> (m.log_r + m.log_c));
-            t[i] = time([&] { hipLaunchKernelGGL(k_once<512>, dim3(ntiles), dim3(512), 72 * 1024, 0, x, y, m); });
-            printf("round %d pass %d R=%d C=%d: %.3f ms %.0f GB/s\n", round, m.pass, 1 << m.log_r, 1 << m.log_c, t[i],
-                   2.0 * n * 16 / t[i] / 1e6);
+    // (A vs W layout orders: profiles/r02_probe_pipe.log.)  The last pass of an
+    // all-worker plan written slice-major (then a separate interleave pass)
+    // vs straight into natural order; plain and nt stores; XCD groups of 8
+    // (k_once loads 16 values x 512 threads = 8192 per tile: only R x C = 8192 maps)
+    const Map maps[] = {{8, 5, 8, 0, 0, 0, 0}, {8, 5, 9, 0, 0, 0, 0}};
+    for (int round = 0; round < 3; round++) {
+        for (uint32_t xg : {2u, 3u}) {
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_log_xg), &xg, 4);
+            for (const Map& m : maps) {
+                const uint32_t ntiles = (uint32_t)(n >> (m.log_r + m.log_c));
+                const float t = time([&] { hipLaunchKernelGGL(k_once<512>, dim3(ntiles), dim3(512), 72 * 1024, 0, x, y, m); });
+                const float tp = time([&] { hipLaunchKernelGGL(k_once_plain<512>, dim3(ntiles), dim3(512), 72 * 1024, 0, x, y, m); });
+                printf("round %d xg %u R=%d C=%d %s: nt %.3f ms %.0f GB/s   plain stores %.3f ms %.0f GB/s\n", round, xg,
+                       1 << m.log_r, 1 << m.log_c, m.pass == 8 ? "slice-major" : "natural   ", t, 2.0 * n * 16 / t / 1e6,
+                       tp, 2.0 * n * 16 / tp / 1e6);
+            }
         }
-        printf("round %d  A total %.3f ms   W total %.3f ms\n", round, t[0] + t[1] + t[2], t[3] + 2 * t[4]);
         fflush(stdout);
     }
     if (hipGetLastError() != hipSuccess) return 2;
