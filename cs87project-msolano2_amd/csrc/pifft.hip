@@ -652,7 +652,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
             s.ta.q0 = p->q0;
             s.ta.nq = p->nq;
             s.block = dim3(256);
-            s.grid = dim3(stride_grid(s.ta.total));
+            s.grid = dim3(stride_grid(s.ta.total / (uint64_t)std::max(1, env_int("PIFFT_TREE_GRID_DIV", 1))));
             s.bytes = (uint64_t)p->batch * esz *
                       (blocks_needed(t0) * (p->n >> t0) + blocks_needed(t0 + L) * (p->n >> (t0 + L)));
             e.steps.push_back(s);
