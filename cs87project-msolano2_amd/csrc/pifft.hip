@@ -553,7 +553,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const size_t esz = p->esz;
     const uint64_t ntrans = (uint64_t)p->batch * p->nq;  // local transforms
     std::vector<PassChoice> passes;
-    const bool may_fuse = p->P > 1 && p->nq == 1 && p->lp <= 4 && env_int("PIFFT_FUSE_TREE", 1);
+    // One worker per plan: the fused pass reads the input once.  Several
+    // workers (the whole transform on one GPU, small N): each worker's pass
+    // re-reads all P leaves, P x the input, which pays only while the input
+    // stays in the Infinity Cache -- PIFFT_FUSE_ALL_MAX_MIB of input
+    // (measured, profiles/r02_fuse_all.log: no consistent win, off by default)
+    const uint64_t in_mib = ((uint64_t)p->batch * p->n * esz) >> 20;
+    const bool fuse_all = p->nq > 1 && in_mib < (uint64_t)env_int("PIFFT_FUSE_ALL_MAX_MIB", 0);
+    const bool may_fuse = p->P > 1 && (p->nq == 1 || fuse_all) && p->lp <= 4 && env_int("PIFFT_FUSE_TREE", 1);
     if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0)) return -1;
     if (p->bitrev && !passes.empty()) {
         // the last pass stores in bit-reversed order: its MODE | 4 twin, at
@@ -693,6 +700,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         if (fuse_here) {
             s.pa.tree = ttw;
             s.pa.worker = p->q0;
+            s.pa.log_nq = (uint32_t)ilog2u(p->nq);
         }
         s.pa.out_bstride = M;
         s.pa.nlines = ntrans * (M >> logr);
@@ -714,7 +722,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
                                                              (unsigned long long)(wgs * k->nt));
         s.grid = dim3((unsigned)wgs);
         s.lds = (size_t)k->lds_bytes;
-        s.bytes = fuse_here ? (uint64_t)p->batch * (p->n + M) * esz : 2 * ntrans * M * esz;
+        s.bytes = fuse_here ? (uint64_t)p->batch * p->nq * (p->n + M) * esz : 2 * ntrans * M * esz;
         if (s.lds > 65536 && !dry)
             (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {

@@ -391,7 +391,9 @@ struct PassArgs {
     // MODE 3 (tree fused into the first pass): worker q of P = 2^LP, leaves
     // x[i + m M], in_bstride = N
     TreeTw tree;
-    uint32_t worker;
+    uint32_t worker;      // first worker of the plan (q0)
+    uint32_t log_nq;      // log2 workers in the plan: transform t of the launch is
+                          // worker q0 + (t mod nq) of batch t / nq (0: one worker)
     // XCD-aware tile order: blocks b and b+8 run on one XCD (shared L2); with
     // log_xg = g > 0, 2^g consecutive tiles (adjacent line groups) are given
     // to blocks of one XCD.  Needs gridDim.x % (8 << g) == 0 (else identity).
@@ -713,7 +715,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             constexpr bool CHUNK = NTS == 2 || NTS == 3;
             const uint64_t j = (CHUNK && a.rd_virt) ? l : global_line<NTS>(a, l);
             const uint32_t les = CHUNK ? a.in_log_es : log_lb;
-            const C2* src = in + bt * a.in_bstride + j + ((uint64_t)b << les);
+            // MODE 3: transform bt is worker (bt mod nq) of batch bt / nq, and
+            // the leaves come from that batch's input
+            const uint64_t bin = BM == 3 ? (bt >> a.log_nq) : bt;
+            const C2* src = in + bin * a.in_bstride + j + ((uint64_t)b << les);
             if constexpr (BM == 3) {
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
@@ -741,7 +746,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     }
                     static_for<0, G, 1>([&](auto gc) {
                         constexpr int g = decltype(gc)::value;
-                        v[u * q + k0 + g] = tree_path_steps<T, LP, q, k0 + g>(w[g], bt, a.worker);
+                        v[u * q + k0 + g] =
+                            tree_path_steps<T, LP, q, k0 + g>(w[g], bt, a.worker + (uint32_t)(tile * C >> log_lb & ((1u << a.log_nq) - 1)));
                     });
                     __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
                 });
