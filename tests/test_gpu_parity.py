@@ -785,3 +785,25 @@ def test_sweep_drives_the_mi355x_cli(tmp_path):
     lines = txt.splitlines()
     assert lines[0].startswith("Empirical time complexity of pi-DFT on NVIDIA GPU (p=8, 2 replications)")
     assert [int(ln.split()[0]) for ln in lines[3:]] == [1 << e for e in range(16, 21)]
+
+
+@pytest.mark.parametrize("suf,logn,P,batch", [("f64", 20, 4, 1), ("f64", 22, 8, 1), ("f32", 20, 8, 1), ("f64", 24, 2, 1), ("f64", 18, 2, 3)])
+def test_fused_tree_all_workers(suf, logn, P, batch, monkeypatch):
+    """The tree fused into the first pass of a plan holding ALL P workers
+    (off by default, PIFFT_FUSE_ALL_MAX_MIB): the worker of each tile comes
+    from its transform index (PassArgs.log_nq).  Same result as the unfused
+    plan and the oracle."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn + P)
+    monkeypatch.setenv("PIFFT_FUSE_ALL_MAX_MIB", "100000")
+    fused = pifft.Plan(n, P, batch, PREC[suf])
+    monkeypatch.delenv("PIFFT_FUSE_ALL_MAX_MIB")
+    plain = pifft.Plan(n, P, batch, PREC[suf])
+    kinds = fused.describe()["launch_kind"]
+    if "tree+pass" not in kinds:
+        pytest.fail(f"no fused instance for this plan: {fused.describe()['radix']} {fused.describe()['lines']} {kinds}")
+    assert plain.describe()["launch_kind"][0] == "tree"
+    got = run(fused, x).reshape(batch, n)
+    assert rel_l2(got.reshape(-1), run(plain, x)) <= tol(suf, n)
+    for bt in range(batch):
+        assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
