@@ -344,6 +344,38 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
     return rec
 
 
+def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev) -> dict:
+    """Configs 2 and 3 on a multi-GPU job, each a timed loop with the headline's
+    barrier + max-over-ranks contract: C2 split one worker per GPU (the
+    reference's 8-way split on real GPUs, P = world), C3's 4096 transforms
+    sharded by transform over the GPUs."""
+    import pifft_dist
+    F64, F32 = pifft.F64, pifft.F32
+    b0, bc = pifft_dist.batch_range(rank, world, 4096)
+    cases = [
+        ("C2_split", f"config 2: fp64 N=2^20 split over {world} GPUs, one worker each (slice-major; "
+                     f"no data-path collective)", 20, F64, dict(P=world, first=rank, count=1, batch_local=1, b_first=0), 1),
+        ("C3_batch", f"config 3: batched fp32 4096 x N=4096 sharded by transform over {world} GPUs",
+         12, F32, dict(P=1, first=0, count=1, batch_local=bc, b_first=b0), 4096),
+    ]
+    out = {}
+    for key, what, log_n, prec, g, batch in cases:
+        rec = {"workload": what}
+        try:
+            job = Job(pifft, torch, gpu, n=1 << log_n, prec=prec, seed=seed, **g)
+            k = max(steps, 50)
+            elapsed = pifft_dist.max_over_ranks(job.run(k, max(warmup, 5), barrier, profile=False), red_dev)
+            ms = elapsed * 1e3 / k
+            rec.update({"value": round(5.0 * (1 << log_n) * log_n * batch / (ms * 1e-3) / 1e9, 2),
+                        "unit": "GFLOP/s", "ms_per_step": round(ms, 6), "steps": k, "n_gpus": world,
+                        "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"]})
+            job.free()
+        except Exception as e:  # reported, never silently replaced
+            rec["error"] = repr(e)
+        out[key] = rec
+    return out
+
+
 def allgather(pifft, torch, dist, job, barrier, red_dev) -> float:
     """The optional final exchange: RCCL all-gather of every rank's slices,
     then the stride-P interleave into natural order on every GPU (ms, max over
@@ -379,7 +411,8 @@ def main() -> int:
                     help="at G > 1, time the optional RCCL all-gather + interleave after the timed region (default)")
     ap.add_argument("--no-allgather", dest="allgather", action="store_false")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip configs 1-3 (at 1 GPU) / config 5 (at 8 GPUs) beside the headline step")
+                    help="skip configs 1-3 (at 1 GPU) / 2-3 split over the GPUs and 5 (at 8 GPUs) beside the "
+                         "headline step")
     ap.add_argument("--c5-log-n", type=int, default=32,
                     help="config 5 size at 8 GPUs (default 2^32; smaller only to rehearse the code path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -478,12 +511,15 @@ def main() -> int:
         if world == 1 and args.log_n == 28 and args.prec == 64 and args.batch == 1:
             secondary = secondary_configs(pifft, torch, gpu, args.steps, args.warmup, args.seed, args.cpu_threads,
                                           not args.no_cpu_baseline)
-        elif world == 8 and args.shard == "workers" and (not args.same_device or args.c5_log_n < 32):
-            try:
-                secondary = {"C5": config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
-                                           min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n)}
-            except Exception as e:  # reported, never silently replaced
-                secondary = {"C5": {"error": repr(e)}}
+        elif world > 1 and args.shard == "workers":
+            secondary = multi_secondary(pifft, torch, dist, gpu, rank, world, args.steps, args.warmup, args.seed,
+                                        barrier, red_dev)
+            if world == 8 and (not args.same_device or args.c5_log_n < 32):
+                try:
+                    secondary["C5"] = config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
+                                              min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n)
+                except Exception as e:  # reported, never silently replaced
+                    secondary["C5"] = {"error": repr(e)}
 
     total_bytes = sum(desc["launch_bytes"][: desc["num_launches"]])
     flops = 5.0 * n * args.log_n * args.batch  # the whole job's batch (every rank's share)

@@ -70,6 +70,29 @@ def test_bench_gpus_2_spawns_two_ranks():
     # the job time is the slowest rank's
     assert d["ms_per_step"] >= max(r["ms_per_step"] for r in pr) * 0.999
     assert d["config"]["allgather_ms"] > 0 and d["cpu_baseline"] is None
+    # configs 2 (one worker per GPU) and 3 (batch-sharded) as multi-GPU loops
+    sec = d["config"]["secondary"]
+    assert set(sec) == {"C2_split", "C3_batch"}
+    for key, rec in sec.items():
+        assert "error" not in rec, (key, rec)
+        assert rec["value"] > 0 and rec["n_gpus"] == 2
+    assert sec["C3_batch"]["batch_per_gpu"] == 2048
+
+
+def test_bench_gpus_8_rehearsal_config5():
+    """The 8-GPU line's code path (the driver's scaling run), rehearsed with 8
+    gloo ranks on one GPU and a small config 5: the headline, configs 2/3 split
+    over the ranks, config 5 and its all-gather all report without error."""
+    d = _bench("--gpus", "8", "--same-device", "--dist-backend", "gloo", "--log-n", "20", "--steps", "2",
+               "--warmup", "1", "--c5-log-n", "22")
+    _common(d, 2, 1, n_gpus=8)
+    assert len(d["config"]["per_rank"]) == 8 and d["config"]["allgather_ms"] > 0
+    sec = d["config"]["secondary"]
+    assert set(sec) == {"C2_split", "C3_batch", "C5"}
+    for key, rec in sec.items():
+        assert "error" not in rec, (key, rec)
+        assert rec["value"] > 0
+    assert sec["C5"]["allgather_ms"] > 0 and sec["C3_batch"]["batch_per_gpu"] == 512
 
 
 def test_bench_secondary_configs():
