@@ -807,3 +807,68 @@ def test_fused_tree_all_workers(suf, logn, P, batch, monkeypatch):
     assert rel_l2(got.reshape(-1), run(plain, x)) <= tol(suf, n)
     for bt in range(batch):
         assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
+
+
+def test_concurrent_plans_from_host_threads():
+    """The shim's threading contract (include/pifft.h; SURVEY.md 8(b)
+    Threading, the reference's P pthreads, CPU.c:336-351): plans are
+    independent objects.  Six host threads each create their own plan and
+    stream and execute it 20 times concurrently (ctypes releases the GIL inside
+    the calls); every result is bitwise the one-thread result.  A seventh
+    thread keeps failing calls: pifft_last_error is per thread, so the workers
+    never see its message."""
+    import threading
+    cases = [(16, 1, "f64", 1), (18, 8, "f64", 1), (17, 4, "f32", 2), (20, 2, "f64", 1), (15, 16, "f32", 3),
+             (19, 1, "f32", 1)]
+    xs, ref = [], []
+    for logn, P, suf, b in cases:
+        x = dev(oracle.generate((1 << logn) * b, DT[suf], seed=logn * 7 + P))
+        p = pifft.Plan(1 << logn, P, b, PREC[suf])
+        y = torch.empty(p.info.out_elems, dtype=x.dtype, device="cuda")
+        p.execute_device(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        xs.append(x)
+        ref.append(y.cpu())
+        p.close()
+    out = [None] * len(cases)
+    errs = []
+    stop = threading.Event()
+
+    def worker(i):
+        try:
+            logn, P, suf, b = cases[i]
+            p = pifft.Plan(1 << logn, P, b, PREC[suf])
+            s = torch.cuda.Stream()
+            y = torch.empty(p.info.out_elems, dtype=xs[i].dtype, device="cuda")
+            with torch.cuda.stream(s):
+                for _ in range(20):
+                    p.execute_device(xs[i].data_ptr(), y.data_ptr(), s)
+            s.synchronize()
+            out[i] = (y.cpu(), pifft.last_error())
+            p.close()
+        except Exception as e:  # surfaced below
+            errs.append(repr(e))
+
+    def failer():
+        p = pifft.Plan(1 << 10, 1, 1, pifft.F64)
+        msgs = set()
+        while not stop.is_set():
+            assert pifft.lib().pifft_execute_device(p.handle, None, None, None) == -1
+            msgs.add(pifft.last_error())
+        out.append(msgs)
+        p.close()
+
+    tf = threading.Thread(target=failer)
+    tf.start()
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(len(cases))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    stop.set()
+    tf.join()
+    assert not errs, errs
+    for i, (y, msg) in enumerate(out[:len(cases)]):
+        assert torch.equal(y, ref[i]), f"case {cases[i]}: concurrent result differs"
+        assert msg == "", f"case {cases[i]}: another thread's error leaked: {msg!r}"
+    assert out[len(cases)] == {"NULL device buffer"}
