@@ -143,6 +143,7 @@ struct pifft_plan {
     size_t esz = 16;
     bool natural = true;
     bool bitrev = false;  // PIFFT_OUT_BITREV
+    bool ilv = false;     // the last pass stores natural order itself (PassArgs::ilv_log)
     std::vector<Step> steps;
     int tree_steps = 0, npasses = 0;
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
@@ -476,7 +477,7 @@ struct Elem {
 int chunk_last_two(pifft_plan* p, const std::vector<PassChoice>& passes, std::vector<Elem>& chain, bool dry) {
     const int chunk_mib = env_int("PIFFT_CHUNK_MIB", 0);
     const size_t k = passes.size();
-    if (chunk_mib <= 0 || k < 3 || p->bitrev || chain.size() < 2) return 0;
+    if (chunk_mib <= 0 || k < 3 || p->bitrev || p->ilv || chain.size() < 2) return 0;
     const PassChoice &ca = passes[k - 2], &cb = passes[k - 1];
     if (ca.mode != 2 || cb.mode != 2 || ca.nts != 1 || cb.nts != 1) return 0;
     const PassKernel* ka = find_pass(p->prec, ca.R, ca.C, 2, 2);
@@ -575,6 +576,33 @@ int build_plan(pifft_plan* p, bool dry = false) {
         l.mode = bm | 4;
     }
 
+    // All P workers on this plan, natural order, and an output small enough to
+    // stay in L2 / the Infinity Cache: the last pass stores each worker's bins
+    // at their natural positions bitrev(q) + P k itself (plain stores; the P
+    // workers' tiles of a line block back to back on one XCD) instead of a
+    // slice-major store plus an interleave launch.  Measured on MI355X
+    // (profiles/r02_ilv_store.log, wall per transform): fp64 2^18-2^22 P=2-16
+    // 1-22 % faster, fp32 2^20 P=8 7 %, batched single-pass plans (4096 x
+    // 4096 fp32 P=4, 1024 x 2^12 fp64 P=4) 13-16 %; 2^23 fp64 and 2^22 fp32
+    // (32 MiB) single transforms up to 5 % slower, few tiles (2^16: 8) 12 %.
+    // PIFFT_ILV: -1 this rule, 0 never, 1 always (where it applies).
+    {
+        const int force = env_int("PIFFT_ILV", -1);
+        const bool ok = p->natural && p->P > 1 && p->nq == p->P && !passes.empty() &&
+                        env_int("PIFFT_CHUNK_MIB", 0) <= 0;
+        bool on = ok && force == 1;
+        if (ok && force < 0) {
+            const PassChoice& l = passes.back();
+            const uint64_t tiles = (ntrans * (p->m / (uint64_t)l.R) + l.C - 1) / (uint64_t)l.C;
+            const uint64_t cap_mib = passes.size() == 1 ? (uint64_t)env_int("PIFFT_ILV_SINGLE_MAX_MIB", 128)
+                                     : p->prec == 64    ? (uint64_t)env_int("PIFFT_ILV_MAX_MIB64", 64)
+                                                        : (uint64_t)env_int("PIFFT_ILV_MAX_MIB32", 16);
+            on = tiles >= (uint64_t)env_int("PIFFT_ILV_MIN_TILES", 256) &&
+                 (uint64_t)p->batch * p->n * esz <= (cap_mib << 20);
+        }
+        p->ilv = on;
+    }
+    if (p->ilv) passes.back().nts = 0;
     TableBuilder tb(esz);
     // --- tree tables (w_N) ---
     const bool need_tree = p->P > 1;
@@ -716,6 +744,11 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.rd_virt = s.pa.wr_virt = 0;
         s.pa.in_log_es = s.pa.log_lb;
         s.pa.out_log_ns = s.pa.log_ns;
+        if (p->ilv && i + 1 == passes.size()) {
+            s.pa.ilv_log = (uint32_t)p->lp;
+            s.pa.out_bstride = p->n;
+            s.pa.log_xg = std::max<uint32_t>(s.pa.log_xg, (uint32_t)env_int("PIFFT_ILV_XCD_GROUP", p->lp));
+        }
         s.block = dim3((unsigned)k->nt);
         const uint64_t wgs = (s.pa.nlines + k->C - 1) / k->C;
         if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
@@ -736,7 +769,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         chain.push_back(e);
     }
     if (chunk_last_two(p, passes, chain, dry)) return -1;
-    if (p->natural && p->P > 1) {
+    if (p->natural && p->P > 1 && !p->ilv) {
         Step s;
         s.kind = STEP_INTERLEAVE;
         s.fn = interleave_fn(p->prec, p->lp, p->n);

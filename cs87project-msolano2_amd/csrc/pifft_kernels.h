@@ -416,6 +416,13 @@ struct PassArgs {
     uint32_t log_sh;
     uint32_t rd_virt, wr_virt;
     uint32_t in_log_es, out_log_ns;
+    // Natural-order store of a plan holding all P = 2^ilv_log workers (its
+    // last pass; 0: the usual slice-major store).  Local transform bt is worker
+    // bt mod P of batch bt / P, and its bin k lands at bitrev(bt mod P) + P k
+    // of that batch's N = out_bstride outputs -- the stride-P interleave done
+    // by the store instead of a separate launch (small N only: 16-B pieces
+    // P x 16 B apart, cheap while the output stays in L2 / the Infinity Cache)
+    uint32_t ilv_log;
 };
 
 // The line map is compiled only into the chunked-pair instances (NTS 2 / 3):
@@ -829,17 +836,22 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 const uint64_t j = (CHUNK && a.wr_virt) ? l : global_line<NTS>(a, l);
                 const uint32_t lns = CHUNK ? a.out_log_ns : (uint32_t)log_ns;
                 const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
-                C2* dst = out + bt * a.out_bstride;
-                if constexpr (BREV) {
+                if constexpr (!BREV) {
+                    // (ilv_log = 0: dst = out + bt out_bstride + pos + k NB 2^lns)
+                    const uint32_t il = a.ilv_log;
+                    const uint64_t rq = il ? (uint64_t)(__builtin_bitreverse32((uint32_t)bt) >> (32 - il)) : 0;
+                    C2* dst = out + (bt >> il) * a.out_bstride + rq + (pos << il);
+                    const uint32_t ks = lns + il;
+#pragma unroll
+                    for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << ks), v[u * q + k]);
+                } else {
+                    C2* dst = out + bt * a.out_bstride;
                     const uint32_t sh = 64 - (log_lb + Sh::LOGR);  // log2 M bits
 #pragma unroll
                     for (int k = 0; k < q; k++) {
                         const uint64_t pk = pos + ((uint64_t)(k * NB) << lns);
                         dst[sh < 64 ? __builtin_bitreverse64(pk) >> sh : 0] = v[u * q + k];
                     }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + pos + ((uint64_t)(k * NB) << lns), v[u * q + k]);
                 }
             }
         }
@@ -911,8 +923,16 @@ void k_pass(PassArgs a) {
     // one tile per workgroup: a persistent tile loop (1, 2 or 4 resident
     // workgroups per CU walking the tiles) measured 1.4-1.7x slower at 2^28
     // fp64
-    pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, reinterpret_cast<T*>(pifft_smem), v, pre, (int)threadIdx.x,
-                                           tile_of_block(blockIdx.x, a.log_xg, gridDim.x));
+    uint64_t tile = tile_of_block(blockIdx.x, a.log_xg, gridDim.x);
+    if (a.ilv_log && a.log_lb >= (uint32_t)ilog2c(C)) {
+        // natural-order store: the P workers' tiles of one line block run
+        // back to back (and on one XCD, log_xg >= log2 P), so the P 16-B
+        // pieces of each output line meet in one L2 before it is written
+        const uint32_t il = a.ilv_log, ltt = a.log_lb - (uint32_t)ilog2c(C);  // 2^ltt tiles per transform
+        const uint64_t q = tile & ((1ull << il) - 1), rest = tile >> il;
+        tile = ((rest >> ltt) << (il + ltt)) + (q << ltt) + (rest & ((1ull << ltt) - 1));
+    }
+    pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, reinterpret_cast<T*>(pifft_smem), v, pre, (int)threadIdx.x, tile);
 }
 
 // ---------------------------------------------------------------------------

@@ -42,7 +42,10 @@ extern "C" {
 #define PIFFT_F64 64
 
 /* plan flags */
-#define PIFFT_OUT_NATURAL 0 /* device output in natural order (needs count == P)   */
+#define PIFFT_OUT_NATURAL 0 /* device output in natural order (needs count == P):
+                               an interleave launch after the last pass, or, for
+                               outputs that stay in L2 / the Infinity Cache, the
+                               last pass storing natural order itself          */
 #define PIFFT_OUT_SLICES 1  /* device output slice-major: worker q's N/P bins
                                Z_q[k] = X[bitrev(q) + P k] contiguous, q = first.. */
 #define PIFFT_OUT_BITREV 2  /* the reference's own scratch order (tmp_in after the

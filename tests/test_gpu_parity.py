@@ -291,7 +291,8 @@ def test_timed_execution_reports_every_launch():
     y = torch.empty(n, dtype=torch.complex128, device="cuda")
     ms = plan.execute_device_timed(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
     assert len(ms) == d["num_launches"] and all(m > 0 for m in ms)
-    assert d["launch_kind"][0] == "tree" and d["launch_kind"][-1] == "interleave"
+    # (the last pass stores natural order itself at this size: no interleave launch)
+    assert d["launch_kind"] == ["tree", "pass", "pass"]
     # asynchronous profiling: events for 3 back-to-back executions, one read
     plan.profile_start(3)
     for _ in range(5):  # only the first 3 are recorded
@@ -872,3 +873,27 @@ def test_concurrent_plans_from_host_threads():
         assert torch.equal(y, ref[i]), f"case {cases[i]}: concurrent result differs"
         assert msg == "", f"case {cases[i]}: another thread's error leaked: {msg!r}"
     assert out[len(cases)] == {"NULL device buffer"}
+
+
+@pytest.mark.parametrize("suf,logn,P,batch", [
+    ("f64", 20, 8, 1), ("f64", 18, 2, 3), ("f64", 21, 16, 1), ("f32", 20, 8, 2), ("f64", 12, 4, 64),
+    ("f32", 12, 8, 33), ("f64", 13, 8, 1), ("f32", 16, 4, 1), ("f64", 22, 8, 1), ("f64", 10, 2, 5)])
+def test_natural_store_in_last_pass(suf, logn, P, batch, monkeypatch):
+    """All-worker plans whose last pass stores natural order itself
+    (PassArgs::ilv_log; PIFFT_ILV=1 forces it where the planner's size rule
+    would not): bitwise equal to the slice-major store + interleave launch
+    (PIFFT_ILV=0), and to the oracle -- multi-pass and single-pass local FFTs,
+    batches, lines per transform below and above the tile's."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn * 3 + P + batch)
+    monkeypatch.setenv("PIFFT_ILV", "1")
+    ilv = pifft.Plan(n, P, batch, PREC[suf])
+    monkeypatch.setenv("PIFFT_ILV", "0")
+    sep = pifft.Plan(n, P, batch, PREC[suf])
+    assert "interleave" not in ilv.describe()["launch_kind"]
+    assert sep.describe()["launch_kind"][-1] == "interleave"
+    got = run(ilv, x)
+    assert got.tobytes() == run(sep, x).tobytes()
+    got = got.reshape(batch, n)
+    for bt in sorted({0, batch - 1}):
+        assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=P, nthreads=8), suf, n)

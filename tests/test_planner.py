@@ -17,8 +17,28 @@ def test_config1_2e20_fp64_one_worker():
 
 def test_config2_2e20_fp64_eight_workers_one_gpu():
     d = pifft.dry_run(1 << 20, 8, 1, F64)
-    assert d["launch_kind"][0] == "tree" and d["launch_kind"][-1] == "interleave"
+    # the last pass stores natural order itself (16 MiB output): no interleave launch
+    assert d["launch_kind"] == ["tree", "pass", "pass"]
     assert d["local_n"] == 1 << 17 and d["out_elems"] == 1 << 20
+
+
+def test_natural_store_rule():
+    """The planner's rule for the last pass storing natural order itself
+    (pifft.hip build_plan, PIFFT_ILV): small outputs with enough tiles; the
+    separate interleave launch above 64 MiB (fp64) / 16 MiB (fp32) and for
+    tiny plans; batched single-pass plans up to 128 MiB."""
+    def kinds(n, P, b, prec):
+        return pifft.dry_run(n, P, b, prec)["launch_kind"]
+    assert kinds(1 << 22, 8, 1, F64)[-1] == "pass"
+    assert kinds(1 << 23, 8, 1, F64)[-1] == "interleave"
+    assert kinds(1 << 20, 8, 1, F32)[-1] == "pass"
+    assert kinds(1 << 22, 8, 1, F32)[-1] == "interleave"
+    assert kinds(1 << 16, 8, 1, F64)[-1] == "interleave"  # 8 tiles
+    assert kinds(4096, 4, 4096, F32)[-1] == "pass"  # single-pass, 128 MiB
+    assert kinds(4096, 4, 8192, F32)[-1] == "interleave"  # 256 MiB
+    assert kinds(1 << 20, 8, 1, F64)[-1] == "pass" and kinds(1 << 20, 1, 1, F64)[-1] == "pass"
+    slices = pifft.dry_run(1 << 20, 8, 1, F64, first=0, count=1)
+    assert "interleave" not in slices["launch_kind"]  # slice plans never interleave
 
 
 def test_config3_batched_fp32_single_pass():
@@ -114,11 +134,13 @@ def test_dry_run_validation():
 def test_bitrev_output_needs_no_interleave(P):
     """PIFFT_OUT_BITREV (the reference's scratch order): the
     whole transform on one GPU skips the interleave launch."""
-    nat = pifft.dry_run(1 << 20, P, 1, F64)
-    d = pifft.dry_run(1 << 20, P, 1, F64, flags=pifft.OUT_BITREV)
+    # (2^23: above the size where natural plans store natural order from their
+    # last pass, so the natural plan has the interleave launch)
+    nat = pifft.dry_run(1 << 23, P, 1, F64)
+    d = pifft.dry_run(1 << 23, P, 1, F64, flags=pifft.OUT_BITREV)
     assert "interleave" not in d["launch_kind"]
     assert d["num_launches"] == nat["num_launches"] - (1 if P > 1 else 0)
-    assert d["out_elems"] == 1 << 20
+    assert d["out_elems"] == 1 << 23
 
 
 def test_bitrev_output_slices_and_bad_flags():
