@@ -798,9 +798,44 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
     }
     if (p->steps.size() > 4096) return fail("plan too large (%zu launches)", p->steps.size());
-    p->bytes_w = need_w ? (size_t)p->batch * p->nq * M * esz : 0;
+    // Padded workspace rows (PassArgs::in_pad / out_pad): where one k_pass
+    // writes W and a later pass (BM 2) reads it, W's rows are spread by
+    // w_pad elements each, so their offsets no longer coincide with the
+    // caller's output rows that the same passes read or write.  Measured on
+    // MI355X over fresh (W, output) allocation pairs (tools/probe_wpad.py,
+    // profiles/r02_wpad.log): C4 fp64 2^28 4.88 -> 4.73 ms mean (worst 5.03
+    // -> 4.82), fp32 2^28 3.22 -> 3.19 ms, with 16 KiB + 256 B per row;
+    // 1 MiB + 256 B ties at fp64 and loses 4 % at fp32.  Only for W >= 2 GiB:
+    // at 512 MiB (fp64 2^25, the worker of 8 at 2^28) padding cost 1.5-2.5 %,
+    // at 1 GiB it ties, at 2 GiB (the worker of 2 at 2^28, of 8 at 2^30) it
+    // gains ~0.5 % (profiles/r02_wpad.log, tools/gpu_wpad_shapes.sh).
+    uint64_t w_tr = M;  // elements per transform in W
+    const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));
+    const uint64_t w_min = (uint64_t)env_int("PIFFT_W_PAD_MIN_MIB", 2048) << 20;
+    if (w_pad && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
+        for (size_t i = 0; i + 1 < p->steps.size(); i++) {
+            Step& a = p->steps[i];
+            Step& b = p->steps[i + 1];
+            if (a.dst != BUF_W || b.src != BUF_W || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
+                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log)
+                continue;
+            const uint64_t rows = M >> b.pa.log_lb;  // the reading pass's radix
+            const uint64_t tr = M + rows * w_pad;
+            const uint32_t logr_a = (uint32_t)(p->log_m - a.pa.log_lb);  // the writing pass's radix
+            a.pa.out_pad = b.pa.in_pad = (uint32_t)w_pad;
+            a.pa.out_pad_log = b.pa.log_lb - logr_a;
+            a.pa.out_bstride = b.pa.in_bstride = tr;
+            w_tr = std::max(w_tr, tr);
+        }
+    }
+    p->bytes_w = need_w ? (size_t)p->batch * p->nq * w_tr * esz : 0;
     if (dry) return 0;
-    if (p->bytes_w) HIPCHK(hipMalloc(&p->buf[BUF_W], p->bytes_w));
+    // tuning knob (tools/probe_place.py): hipExtMallocWithFlags flags for the
+    // ping-pong workspace, e.g. 4 = hipDeviceMallocContiguous
+    const int w_flags = env_int("PIFFT_W_MALLOC_FLAGS", 0);
+    if (p->bytes_w)
+        HIPCHK(w_flags ? hipExtMallocWithFlags(&p->buf[BUF_W], p->bytes_w, (unsigned)w_flags)
+                       : hipMalloc(&p->buf[BUF_W], p->bytes_w));
     if (p->bytes_ta) HIPCHK(hipMalloc(&p->buf[BUF_TA], p->bytes_ta));
     if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
     if (p->bytes_ch) HIPCHK(hipMalloc(&p->buf[BUF_CH], p->bytes_ch));

@@ -423,6 +423,18 @@ struct PassArgs {
     // by the store instead of a separate launch (small N only: 16-B pieces
     // P x 16 B apart, cheap while the output stays in L2 / the Infinity Cache)
     uint32_t ilv_log;
+    // Padded workspace rows (the plan's ping-pong buffer W between two
+    // passes; 0 elsewhere).  Element e of a W transform sits at
+    // e + (e >> s) pad, s = log2 of the reading pass's row stride: the
+    // reading pass (BM 2) steps its R rows by 2^log_lb + in_pad, the writing
+    // pass adds (j >> out_pad_log) out_pad to every store of line j (its
+    // outputs e >> s all equal j >> (s - log2 R): a Stockham pass's output
+    // blocks Ns R never straddle the next pass's rows, Ns R <= M / R').
+    // Unpadded, the rows of W and of the caller's output sit at the same
+    // offsets, 8 MiB apart at 2^28 fp64, and the C4 passes 2 and 3 ran fast
+    // or slow (pass 3 1.58 vs 1.70-1.86 ms) by how the two allocations
+    // happened to line up (tools/probe_place.py, tools/probe_pair.hip).
+    uint32_t in_pad, out_pad, out_pad_log;
 };
 
 // The line map is compiled only into the chunked-pair instances (NTS 2 / 3):
@@ -758,6 +770,13 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     });
                     __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
                 });
+            } else if constexpr (BM == 2 && !CHUNK) {
+                // rows 2^les + in_pad apart (padded workspace, PassArgs::in_pad)
+                const uint64_t rs = (1ull << les) + a.in_pad;
+                const C2* row = in + bin * a.in_bstride + j + (uint64_t)b * rs;
+#pragma unroll
+                for (int k = 0; k < q; k++)
+                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs) : C2{(T)0, (T)0};
             } else {
 #pragma unroll
                 for (int k = 0; k < q; k++)
@@ -840,7 +859,9 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     // (ilv_log = 0: dst = out + bt out_bstride + pos + k NB 2^lns)
                     const uint32_t il = a.ilv_log;
                     const uint64_t rq = il ? (uint64_t)(__builtin_bitreverse32((uint32_t)bt) >> (32 - il)) : 0;
-                    C2* dst = out + (bt >> il) * a.out_bstride + rq + (pos << il);
+                    // (out_pad: the line block's offset in a padded workspace)
+                    const uint64_t pad = CHUNK ? 0 : (j >> a.out_pad_log) * a.out_pad;
+                    C2* dst = out + (bt >> il) * a.out_bstride + rq + (pos << il) + pad;
                     const uint32_t ks = lns + il;
 #pragma unroll
                     for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << ks), v[u * q + k]);

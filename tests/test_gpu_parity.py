@@ -897,3 +897,36 @@ def test_natural_store_in_last_pass(suf, logn, P, batch, monkeypatch):
     got = got.reshape(batch, n)
     for bt in sorted({0, batch - 1}):
         assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=P, nthreads=8), suf, n)
+
+
+@pytest.mark.parametrize("suf,logn,P,first,count,batch,flags", [
+    ("f64", 20, 1, 0, 1, 1, pifft.OUT_NATURAL),   # two passes: pass 1 writes W, pass 2 reads it
+    ("f64", 22, 1, 0, 1, 1, pifft.OUT_NATURAL),   # three passes: W between passes 2 and 3
+    ("f32", 24, 1, 0, 1, 1, pifft.OUT_NATURAL),
+    ("f64", 18, 1, 0, 1, 3, pifft.OUT_NATURAL),   # batch: padded transform stride
+    ("f64", 21, 8, 5, 1, 1, pifft.OUT_SLICES),    # fused tree pass writes W
+    ("f64", 22, 4, 2, 2, 2, pifft.OUT_SLICES),    # worker range + batch
+    ("f64", 20, 8, 0, 8, 1, pifft.OUT_NATURAL),   # tree + passes + natural store
+    ("f64", 24, 16, 3, 1, 1, pifft.OUT_SLICES),   # worker of 16 (fused tree, multi-pass)
+    ("f64", 20, 1, 0, 1, 1, pifft.OUT_BITREV),    # bit-reversed last pass reads W
+])
+@pytest.mark.parametrize("pad", [1040, 37])
+def test_padded_workspace_rows(suf, logn, P, first, count, batch, flags, pad, monkeypatch):
+    """Padded workspace rows forced onto small plans (PIFFT_W_PAD_MIN_MIB=0;
+    by default only W beyond the Infinity Cache is padded): bitwise equal to
+    the unpadded plan (PIFFT_W_PAD=0) and to the oracle, for every hand-off
+    through W (first pass, later pass, fused tree pass, batches, worker
+    ranges, bit-reversed output) and an odd pad."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn + 7 * P + batch)
+    monkeypatch.setenv("PIFFT_W_PAD_MIN_MIB", "0")
+    monkeypatch.setenv("PIFFT_W_PAD", str(pad))
+    padded = pifft.Plan(n, P, batch, PREC[suf], first=first, count=count, flags=flags)
+    monkeypatch.setenv("PIFFT_W_PAD", "0")
+    plain = pifft.Plan(n, P, batch, PREC[suf], first=first, count=count, flags=flags)
+    assert padded.describe()["workspace_bytes"] > plain.describe()["workspace_bytes"]
+    got = run(padded, x)
+    assert got.tobytes() == run(plain, x).tobytes()
+    if flags == pifft.OUT_NATURAL:
+        got = got.reshape(batch, n)
+        assert_bins_close(got[-1], oracle.fft(x[(batch - 1) * n:], P=P, nthreads=8), suf, n)

@@ -161,3 +161,23 @@ def test_every_multipass_worker_plan_fuses_its_tree(prec):
             d = pifft.dry_run(1 << logn, P, 1, prec, first=P - 1, count=1)
             if d["num_passes"] > 1:
                 assert d["launch_kind"][0] == "tree+pass", (logn, P, d["radix"], d["lines"])
+
+
+def test_padded_workspace_rows(monkeypatch):
+    """Padded workspace rows (PassArgs::in_pad/out_pad, PIFFT_W_PAD): W rows
+    16 KiB + 256 B apart for a W of 2 GiB or more (C4: 512 rows of pass 3),
+    none below (the worker of 8 at 2^28: 512 MiB); PIFFT_W_PAD=0 turns it off."""
+    def ws(n, P=1, prec=F64, **kw):
+        return pifft.dry_run(n, P, 1, prec, **kw)["workspace_bytes"]
+    padded = ws(1 << 28)
+    monkeypatch.setenv("PIFFT_W_PAD", "0")
+    assert padded - ws(1 << 28) == 512 * 1040 * 16
+    # fp32 2^28 (four passes 128^4): both workspace hand-offs read 128 rows
+    monkeypatch.delenv("PIFFT_W_PAD")
+    padded32 = ws(1 << 28, prec=F32)
+    monkeypatch.setenv("PIFFT_W_PAD", "0")
+    assert padded32 - ws(1 << 28, prec=F32) == 128 * 2080 * 8
+    monkeypatch.delenv("PIFFT_W_PAD")
+    small = ws(1 << 28, 8, first=0, count=1, flags=pifft.OUT_SLICES)
+    monkeypatch.setenv("PIFFT_W_PAD", "0")
+    assert small == ws(1 << 28, 8, first=0, count=1, flags=pifft.OUT_SLICES)
