@@ -22,7 +22,7 @@ import pifft  # noqa: E402
 LOG_N = int(os.environ.get("PROBE_LOG_N", "28"))
 PREC = int(os.environ.get("PROBE_PREC", "64"))
 TRIALS = int(os.environ.get("PROBE_TRIALS", "5"))
-PADS = [int(v) for v in os.environ.get("PROBE_PADS", "0,16,272,1040,8208,65552").split(",")]
+PADS = os.environ.get("PROBE_PADS", "0,16,272,1040,8208,65552").split(",")
 P = int(os.environ.get("PROBE_P", "1"))  # workers; the plan holds worker 0 only when P > 1
 STEPS = 8
 
@@ -43,7 +43,9 @@ def main():
         keep.append(y)
         row = []
         for pad in PADS:
-            os.environ["PIFFT_W_PAD"] = str(pad)
+            # "<pad>ip": the last pass in place in the output (PIFFT_INPLACE_LAST)
+            os.environ["PIFFT_W_PAD"] = pad[:-2] if pad.endswith("ip") else pad
+            os.environ["PIFFT_INPLACE_LAST"] = "1" if pad.endswith("ip") else "0"
             plan = pifft.Plan(n, P, 1, prec, first=0, count=1, device=0,
                               flags=pifft.OUT_NATURAL if P == 1 else pifft.OUT_SLICES)
             best = None
@@ -70,7 +72,7 @@ def main():
         print(f"trial {t}: " + "  ".join(row), flush=True)
     for pad in PADS:
         v = sums_by_pad[pad]
-        print(f"pad {pad:6d}: mean {sum(v) / len(v):.3f} ms  min {min(v):.3f}  max {max(v):.3f}", flush=True)
+        print(f"pad {pad:>8s}: mean {sum(v) / len(v):.3f} ms  min {min(v):.3f}  max {max(v):.3f}", flush=True)
 
 
 if __name__ == "__main__":
