@@ -113,39 +113,10 @@ const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int l
     return nullptr;
 }
 
-// Two-pass plans in one launch (k_pass2): first pass (mode 1) + later pass of
-// the same thread count, for the cache-resident sizes where a launch's ramp
-// and drain are a large share of a pass (C1: fp64 2^20, 2 x 1024-point passes)
-struct Pass2Kernel {
-    int prec, R1, C1, nts, R2, C2;
-    const void* fn;
-    int nt, lds_bytes;
-};
-#define PK2(T, PREC, R1, C1, NTS, R2, C2)                                                                     \
-    Pass2Kernel {                                                                                              \
-        PREC, R1, C1, NTS, R2, C2, reinterpret_cast<const void*>(&k_pass2<T, R1, C1, 1, NTS, 0, R2, C2>),    \
-            PassCfg<R1, C1>::NT,                                                                               \
-            std::max(pass_lds_bytes<T, R1, C1, 1, 16>(), pass_lds_bytes<T, R2, C2, 2, 16>())                  \
-    }
-const Pass2Kernel kPass2[] = {
-    PK2(double, 64, 1024, 4, 1, 1024, 4), PK2(double, 64, 1024, 4, 0, 1024, 4),
-    PK2(double, 64, 512, 4, 0, 512, 4),   PK2(double, 64, 256, 4, 0, 256, 4),
-    PK2(float, 32, 1024, 4, 1, 1024, 4),  PK2(float, 32, 1024, 4, 0, 1024, 4),
-    PK2(float, 32, 512, 4, 0, 512, 4),    PK2(float, 32, 256, 4, 0, 256, 4),
-};
-#undef PK2
-
-const Pass2Kernel* find_pass2(int prec, int R1, int C1, int nts, int R2, int C2) {
-    for (const auto& k : kPass2)
-        if (k.prec == prec && k.R1 == R1 && k.C1 == C1 && k.nts == nts && k.R2 == R2 && k.C2 == C2) return &k;
-    return nullptr;
-}
-
 // ---------------------------------------------------------------------------
 // plan
 // ---------------------------------------------------------------------------
-enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4, STEP_CHUNK_A = 5, STEP_CHUNK_B = 6,
-       STEP_PASS2 = 7 };
+enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4, STEP_CHUNK_A = 5, STEP_CHUNK_B = 6 };
 enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, BUF_CH = 5, NBUF = 6 };
 
 struct Step {
@@ -156,10 +127,6 @@ struct Step {
     int src = -1, dst = -2;  // -1 / -2: the chain element's input / output buffer
     uint64_t src_off = 0, dst_off = 0;  // elements
     PassArgs pa{};
-    PassArgs pa2{};                   // STEP_PASS2: the second pass (pa: the first)
-    int mid = -1;                     // STEP_PASS2: the buffer between the two passes
-    bool coop_plain = false;          // STEP_PASS2: hipLaunchKernel instead of the cooperative launch
-    const PassKernel* pk = nullptr;   // STEP_PASS / STEP_TREE_PASS: the instance
     TreeArgs ta{};
     uint64_t il_total = 0;
     uint32_t il_log_n = 0, il_log_p = 0;
@@ -194,7 +161,6 @@ struct pifft_plan {
     void* d_hin = nullptr;   // pifft_execute's staging copies
     void* d_hout = nullptr;
     void* d_gather = nullptr;  // pifft_allgather: every worker's slices on this plan's device
-    uint32_t* d_bar = nullptr; // k_pass2's grid barrier words (STEP_PASS2)
     std::vector<char> host_tmp;
     std::vector<int> peer_on;  // devices this plan's device has peer access to (pifft_allgather)
     std::vector<hipStream_t> gst;  // pifft_allgather: one copy stream per source plan
@@ -482,7 +448,6 @@ void release(pifft_plan* p) {
     if (p->d_hin) (void)hipFree(p->d_hin);
     if (p->d_hout) (void)hipFree(p->d_hout);
     if (p->d_gather) (void)hipFree(p->d_gather);
-    if (p->d_bar) (void)hipFree(p->d_bar);
     for (auto st : p->gst) (void)hipStreamDestroy(st);
     for (auto e : p->gdone) (void)hipEventDestroy(e);
     for (auto e : p->gev)
@@ -754,7 +719,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
         s.fn = k->fn;
-        s.pk = k;
         const int logr = ilog2u((uint64_t)k->R);
         s.pa.tw_r = twp(tw_r[i]);
         s.pa.tw_lo = passes.size() > 1 ? twp(pass2.lo) : nullptr;
@@ -865,48 +829,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
     }
     p->bytes_w = need_w ? (size_t)p->batch * p->nq * w_tr * esz : 0;
-    // Two passes in one launch (k_pass2, PIFFT_COOP): a plan of exactly a
-    // first and a later pass with an instance, whose tiles all fit on the chip
-    // at once (<= one workgroup per CU; checked against the device's
-    // occupancy below and launched cooperatively).
-    if (p->steps.size() == 2 && env_int("PIFFT_COOP", 0) > 0) {
-        const Step& a = p->steps[0];
-        const Step& b = p->steps[1];
-        const Pass2Kernel* k2 = nullptr;
-        if (a.kind == STEP_PASS && b.kind == STEP_PASS && a.pk && b.pk && a.pk->mode == 1 && b.pk->mode == 2 &&
-            a.pk->nts == b.pk->nts && a.dst == b.src && !b.pa.ilv_log)
-            k2 = find_pass2(p->prec, a.pk->R, a.pk->C, a.pk->nts, b.pk->R, b.pk->C);
-        const uint32_t grid = std::max(a.grid.x, b.grid.x);
-        if (k2 && grid <= (uint32_t)env_int("PIFFT_COOP_MAX_WG", 256)) {
-            int per_cu = 0, cus = 0;
-            bool fits = dry;
-            if (!dry && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k2->fn, k2->nt, k2->lds_bytes) ==
-                            hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess)
-                fits = (uint64_t)per_cu * (uint64_t)cus >= grid;
-            if (fits) {
-                Step m = a;
-                m.kind = STEP_PASS2;
-                m.coop_plain = env_int("PIFFT_COOP", 0) == 2;
-                m.fn = k2->fn;
-                m.pk = nullptr;
-                m.pa2 = b.pa;
-                m.mid = a.dst;
-                m.dst = b.dst;
-                m.grid = dim3(grid);
-                m.lds = (size_t)k2->lds_bytes;
-                m.bytes = a.bytes + b.bytes;
-                p->steps.assign(1, m);
-            }
-        }
-    }
     if (dry) return 0;
-    if (!p->steps.empty() && p->steps[0].kind == STEP_PASS2) {
-        HIPCHK(hipMalloc(&p->d_bar, 4 * sizeof(uint32_t)));
-        HIPCHK(hipMemset(p->d_bar, 0, 4 * sizeof(uint32_t)));
-        if (p->steps[0].lds > 65536)
-            (void)hipFuncSetAttribute(p->steps[0].fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->steps[0].lds);
-    }
     // tuning knob (tools/probe_place.py): hipExtMallocWithFlags flags for the
     // ping-pong workspace, e.g. 4 = hipDeviceMallocContiguous
     const int w_flags = env_int("PIFFT_W_MALLOC_FLAGS", 0);
@@ -993,19 +916,6 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             a.out = dst;
             void* args[] = {&a};
             e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
-            break;
-        }
-        case STEP_PASS2: {
-            PassArgs a = s.pa, b = s.pa2;
-            a.in = src;
-            a.out = base[s.mid];
-            b.in = base[s.mid];
-            b.out = dst;
-            uint32_t* bar = p->d_bar;
-            void* args[] = {&a, &b, &bar};
-            // PIFFT_COOP=2: a plain launch (the grid is co-resident by the planner's check)
-            e = s.coop_plain ? hipLaunchKernel(s.fn, s.grid, s.block, args, s.lds, st)
-                             : hipLaunchCooperativeKernel(s.fn, s.grid, s.block, args, (unsigned)s.lds, st);
             break;
         }
         case STEP_INTERLEAVE: {

@@ -957,69 +957,6 @@ void k_pass(PassArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Both passes of a two-pass plan in ONE launch (small, cache-resident sizes)
-// ---------------------------------------------------------------------------
-// Grid-wide barrier between the passes.  bar[0]: arrivals of this launch
-// (reset by the last arrival), bar[1]: generation, bar[2]: set if a wave gave
-// up waiting.  The planner only merges passes whose grid fits on the chip at
-// once (all workgroups co-resident), so the wait always ends; the bounded
-// spin is a guard only.  Memory: __syncthreads() completes every wave's
-// pass-1 stores to the L2; thread 0's agent-scope release then writes its
-// XCD's L2 back before the arrival, and its agent-scope acquire after the
-// wait invalidates the CU's L1 and the XCD's L2, so the pass-2 loads of any
-// XCD see every workgroup's stores.  (A release/acquire fence in every
-// thread -- 65536 L2 write-backs at 2^20 -- made the launch 5x slower.)
-// Vector atomics only.
-__device__ __forceinline__ void grid_sync(uint32_t* bar, uint32_t nblocks) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const uint32_t gen = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1) {
-            __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&bar[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            for (uint32_t spin = 0;
-                 __hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen; spin++) {
-                if (spin >= (1u << 22)) {
-                    __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-}
-
-// Pass 1 (MODE M1: 1 strided first pass, 3 with the tree fused in) of a
-// two-pass plan, the grid barrier, then pass 2 (MODE 2), on the same
-// workgroups: one launch instead of two for plans small enough that every
-// tile of a pass is resident at once (C1, fp64 2^20: 256 tiles).  Both passes
-// run with the same thread count; a workgroup whose tile lies past a pass's
-// lines runs that pass with every load and store guarded off.
-template <typename T, int R1, int C1, int M1, int NTS, int LP, int R2, int C2>
-__global__ __launch_bounds__((PassCfg<R1, C1>::NT), (PassCfg<R1, C1>::waves_per_eu))
-void k_pass2(PassArgs a1, PassArgs a2, uint32_t* bar) {
-    static_assert(PassCfg<R1, C1>::NT == PassCfg<R2, C2>::NT, "both passes on the same workgroup");
-    extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem2[];
-    T* lds = reinterpret_cast<T*>(pifft_smem2);
-    const int tid = (int)threadIdx.x;
-    {
-        cx<T> v[PassShape<R1>::Q];
-        cx<T> pre[pre_count<R1, C1, M1, 16>() > 0 ? pre_count<R1, C1, M1, 16>() : 1];
-        pass_stages<T, R1, C1, M1, NTS, LP, 0, 16>(a1, lds, v, pre, tid, tile_of_block(blockIdx.x, a1.log_xg, gridDim.x));
-    }
-    grid_sync(bar, gridDim.x);
-    {
-        cx<T> v[PassShape<R2>::Q];
-        cx<T> pre[pre_count<R2, C2, 2, 16>() > 0 ? pre_count<R2, C2, 2, 16>() : 1];
-        pass_stages<T, R2, C2, 2, NTS, 0, 0, 16>(a2, lds, v, pre, tid, tile_of_block(blockIdx.x, a2.log_xg, gridDim.x));
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Tree ("funnel") stage
 // ---------------------------------------------------------------------------
 // Levels t0 .. t0+L-1 of the reference's radix-2 tree (CPU.c:419-448, level t

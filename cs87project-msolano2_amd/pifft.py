@@ -20,7 +20,7 @@ CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64
 OUT_NATURAL, OUT_SLICES, OUT_BITREV = 0, 1, 2
-KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass", 5: "chunk-a", 6: "chunk-b", 7: "pass2"}
+KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass", 5: "chunk-a", 6: "chunk-b"}
 MAX_LAUNCH_INFO = 256  # PIFFT_MAX_LAUNCH_INFO (include/pifft.h)
 
 

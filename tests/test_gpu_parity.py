@@ -930,31 +930,3 @@ def test_padded_workspace_rows(suf, logn, P, first, count, batch, flags, pad, mo
     if flags == pifft.OUT_NATURAL:
         got = got.reshape(batch, n)
         assert_bins_close(got[-1], oracle.fft(x[(batch - 1) * n:], P=P, nthreads=8), suf, n)
-
-
-@pytest.mark.parametrize("suf,logn,batch", [("f64", 20, 1), ("f64", 18, 1), ("f64", 16, 1), ("f32", 20, 1),
-                                            ("f64", 16, 4), ("f32", 16, 4)])
-def test_two_passes_one_launch(suf, logn, batch, monkeypatch):
-    """Two-pass plans as ONE cooperative launch (k_pass2: first pass, grid
-    barrier, second pass; PIFFT_COOP=1): bitwise equal to the two-launch plan
-    and within tolerance of the oracle, also after many back-to-back
-    executions (the barrier words are reused launch after launch)."""
-    n = 1 << logn
-    x = oracle.generate(n * batch, DT[suf], seed=logn + batch)
-    monkeypatch.setenv("PIFFT_COOP", "1")
-    one = pifft.Plan(n, 1, batch, PREC[suf])
-    monkeypatch.setenv("PIFFT_COOP", "0")
-    two = pifft.Plan(n, 1, batch, PREC[suf])
-    assert one.describe()["launch_kind"] == ["pass2"]
-    assert two.describe()["launch_kind"] == ["pass", "pass"]
-    want = run(two, x)
-    assert run(one, x).tobytes() == want.tobytes()
-    d_in = dev(x)
-    d_out = torch.empty_like(d_in)
-    s = torch.cuda.current_stream()
-    for _ in range(300):
-        one.execute_device(d_in.data_ptr(), d_out.data_ptr(), s)
-    torch.cuda.synchronize()
-    assert d_out.cpu().numpy().tobytes() == want.tobytes()
-    got = want.reshape(batch, n)
-    assert_bins_close(got[-1], oracle.fft(x[(batch - 1) * n:], P=1), suf, n)
