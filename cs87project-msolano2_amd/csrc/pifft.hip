@@ -127,6 +127,7 @@ struct Step {
     int src = -1, dst = -2;  // -1 / -2: the chain element's input / output buffer
     uint64_t src_off = 0, dst_off = 0;  // elements
     PassArgs pa{};
+    int nts = 0;  // STEP_PASS / STEP_TREE_PASS: the instance's streaming form (2, 3: chunked-pair instances)
     TreeArgs ta{};
     uint64_t il_total = 0;
     uint32_t il_log_n = 0, il_log_p = 0;
@@ -719,6 +720,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
         s.fn = k->fn;
+        s.nts = k->nts;
         const int logr = ilog2u((uint64_t)k->R);
         s.pa.tw_r = twp(tw_r[i]);
         s.pa.tw_lo = passes.size() > 1 ? twp(pass2.lo) : nullptr;
@@ -817,7 +819,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
             if (a.dst != BUF_W || b.src != BUF_W || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
-                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log)
+                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log ||
+                a.nts == 2 || a.nts == 3 || b.nts == 2 || b.nts == 3)  // chunked-pair instances: unpadded only
                 continue;
             const uint64_t rows = M >> b.pa.log_lb;  // the reading pass's radix
             const uint64_t tr = M + rows * w_pad;
