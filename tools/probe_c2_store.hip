@@ -8,6 +8,10 @@
 //   slice : tile of worker q reads q 2^17 + j + 512 r, writes the same index
 //   inter : the interleave: out[bitrev3(q) + 8 k] = in[q 2^17 + k]
 //   nat   : the pass writing (j + 512 r) 8 + bitrev3(q) directly
+//   wi<CW>: (round 2, second form) a "worker-interleaved" tile: CW lines of
+//           ALL 8 workers per workgroup, loaded CW x 16 B at a time per worker
+//           row, stored with the 8 workers' values of one output adjacent
+//           (8 x CW consecutive natural outputs per row, coalesced)
 //   hipcc -O3 -w --offload-arch=gfx950 tools/probe_c2_store.hip -o tools/probe_c2_store
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,6 +38,23 @@ __global__ __launch_bounds__(128) void k_last(const d2* __restrict__ in, d2* __r
         d2* p = NAT ? out + (e << 3) + brev3(q) : out + ((uint64_t)q << 17) + e;
         if (NT_ST) __builtin_nontemporal_store(v[k], p);
         else *p = v[k];
+    }
+}
+
+template <int CW>
+__global__ __launch_bounds__(128 * CW) void k_wi(const d2* __restrict__ in, d2* __restrict__ out) {
+    constexpr int NT = 128 * CW;
+    const uint32_t t = blockIdx.x;  // lines t CW .. t CW + CW - 1 of every worker
+    d2 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int g = threadIdx.x + NT * k, cw = g % CW, q = (g / CW) & 7, r = g / (8 * CW);
+        v[k] = __builtin_nontemporal_load(in + ((uint64_t)q << 17) + t * CW + cw + 512 * r);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int g = threadIdx.x + NT * k, q = g & 7, cw = (g >> 3) % CW, r = g / (8 * CW);
+        out[((uint64_t)(t * CW + cw + 512 * r) << 3) + brev3(q)] = v[k];
     }
 }
 
@@ -71,8 +92,12 @@ int main() {
         });
         const float b1 = time([&] { hipLaunchKernelGGL((k_last<1, 1>), dim3(512), dim3(128), 0, 0, x, z); });
         const float b0 = time([&] { hipLaunchKernelGGL((k_last<1, 0>), dim3(512), dim3(128), 0, 0, x, z); });
-        printf("round %d (us): last pass slice-major %.2f, + interleave launch %.2f | natural store nt %.2f, plain %.2f\n",
-               round, a, ai, b1, b0);
+        const float w1 = time([&] { hipLaunchKernelGGL(k_wi<1>, dim3(512), dim3(128), 0, 0, x, z); });
+        const float w2 = time([&] { hipLaunchKernelGGL(k_wi<2>, dim3(256), dim3(256), 0, 0, x, z); });
+        const float w4 = time([&] { hipLaunchKernelGGL(k_wi<4>, dim3(128), dim3(512), 0, 0, x, z); });
+        printf("round %d (us): last pass slice-major %.2f, + interleave launch %.2f | natural store nt %.2f, plain %.2f"
+               " | worker-interleaved tile CW=1 %.2f, CW=2 %.2f, CW=4 %.2f\n",
+               round, a, ai, b1, b0, w1, w2, w4);
         fflush(stdout);
     }
     return hipGetLastError() != hipSuccess ? 2 : 0;
