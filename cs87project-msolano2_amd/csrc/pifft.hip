@@ -968,20 +968,12 @@ void stage_split(const pifft_plan* p, const std::vector<float>& ms, double* s1, 
     if (s2) *s2 = b;
 }
 
-// device result (slice-major or natural) -> natural-order host positions
+// device result of a plan holding only some workers (slice-major) -> their
+// natural-order host positions (natural-order and bit-reversed plans copy
+// straight into host_out, pifft_execute_group)
 void scatter_to_host(const pifft_plan* p, const char* res, char* host_out) {
     const size_t esz = p->esz;
-    if (p->natural) {
-        memcpy(host_out, res, (size_t)p->batch * p->n * esz);
-        return;
-    }
     const uint64_t M = p->m;
-    if (p->bitrev) {  // the reference's tmp_in layout: segments at q M
-        for (uint32_t bt = 0; bt < p->batch; bt++)
-            memcpy(host_out + ((uint64_t)bt * p->n + (uint64_t)p->q0 * M) * esz,
-                   res + (uint64_t)bt * p->nq * M * esz, (size_t)p->nq * M * esz);
-        return;
-    }
     // a plan holding only some workers: its bins go to their stride-P
     // natural-order positions (other positions untouched, CPU.c:496-499);
     // typed element copies (one 8/16-B move each, not a memcpy call)
@@ -1351,6 +1343,22 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
         for (int i = 0; i < np; i++) {
             pifft_plan* p = plans[i];
             DeviceGuard g(p->device);
+            // natural order, and the reference's scratch order (whole segments),
+            // land in host_out as they are: straight device-to-host copies (no
+            // host-side staging copy: that single-threaded 4 GiB memcpy was half
+            // of a 2^28 fp64 call, profiles/r02_host_boundary.log)
+            if (p->natural) {
+                HIPCHK(hipMemcpy(host_out, p->d_hout, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToHost));
+                continue;
+            }
+            if (p->bitrev) {
+                const uint64_t M = p->m;
+                for (uint32_t bt = 0; bt < p->batch; bt++)
+                    HIPCHK(hipMemcpy((char*)host_out + ((uint64_t)bt * p->n + (uint64_t)p->q0 * M) * p->esz,
+                                     (const char*)p->d_hout + (uint64_t)bt * p->nq * M * p->esz,
+                                     (size_t)p->nq * M * p->esz, hipMemcpyDeviceToHost));
+                continue;
+            }
             const size_t bytes = (size_t)out_elems(p) * p->esz;
             p->host_tmp.resize(bytes);
             HIPCHK(hipMemcpy(p->host_tmp.data(), p->d_hout, bytes, hipMemcpyDeviceToHost));
