@@ -165,7 +165,10 @@ int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double*
  * the P-GPU no-communication split.  Stage times are the max over plans.
  * When the plans hold all P workers between them (PIFFT_OUT_SLICES), host_out
  * is filled through pifft_allgather onto the first plan's device and one
- * device-to-host copy; otherwise each plan's bins are scattered on the host. */
+ * device-to-host copy; otherwise a plan whose output is natural order or the
+ * reference's scratch order (PIFFT_OUT_BITREV) is copied straight into
+ * host_out, and a plan holding only some workers has its bins scattered on
+ * the host. */
 int pifft_execute_group(pifft_plan** plans, int nplans, const void* host_in, void* host_out,
                         double* ms_stage1, double* ms_stage2);
 
