@@ -1,4 +1,6 @@
 #!/bin/bash
+# (PIFFT_INPLACE_LAST was an A/B knob, removed after this measurement -- profiles/r02_wpad.log; the
+# script is kept as the record of how the numbers were taken.)
 # tools/gpu_inplace_ab.sh -- A/B of the last pass in place (PIFFT_INPLACE_LAST):
 # C4 over fresh (W, y) pairs, then the small plans (C1 2^20, 2^22, C2 slice).
 set -o pipefail
