@@ -60,7 +60,7 @@ def test_random_plan_vs_oracle(suf, logn, P, first, count, batch, flags):
     got = d_out.cpu().numpy()
     per = got.size // batch
     for b in sorted({0, batch - 1}):
-        X = oracle.fft(xs[b], P=P, nthreads=8)
+        X = oracle.fft(xs[b], P=P, nthreads=16)
         g = got[b * per:(b + 1) * per]
         if flags == pifft.OUT_NATURAL:
             assert_bins_close(g, X, suf, n)
@@ -89,3 +89,25 @@ def test_random_plan_padded_workspace_bitwise(suf, logn, P, first, count, batch,
         torch.cuda.synchronize()
         outs.append(d_out.cpu().numpy().tobytes())
     assert outs[0] == outs[1]
+
+
+def _large_cases(count=8, seed=4242):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(count):
+        suf = rng.choice(["f32", "f64"])
+        logn = rng.randint(22, 24)
+        P = 1 << rng.randint(0, 4)
+        flags = rng.choice([pifft.OUT_NATURAL, pifft.OUT_SLICES, pifft.OUT_BITREV])
+        cnt = P if flags == pifft.OUT_NATURAL else 1 << rng.randint(0, P.bit_length() - 1)
+        first = 0 if flags == pifft.OUT_NATURAL else cnt * rng.randrange(P // cnt)
+        out.append((suf, logn, P, first, cnt, 1, flags))
+    return out
+
+
+@pytest.mark.parametrize("suf,logn,P,first,count,batch,flags", _large_cases())
+def test_random_large_plan_vs_oracle(suf, logn, P, first, count, batch, flags):
+    """Seeded random multi-pass shapes at N = 2^22..2^24 (three-pass local
+    FFTs, the natural-store and interleave rules, fused trees), vs the oracle
+    on 16 host threads."""
+    test_random_plan_vs_oracle(suf, logn, P, first, count, batch, flags)
