@@ -56,7 +56,15 @@ sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-CPU_MEM_CAP = 160 << 30  # never plan a CPU sample above this (the GPU box caps a command near 270 GiB)
+# The reference's own processor sweep: p = 1 .. 32 (run-experiments-and-analyze-
+# results:29, p_to=32), skipping p above the machine's online CPUs
+# (how-many-cpu-cores.c; CPU.c:200, 835-837 refuses p > sysconf(ONLN))
+REF_P_TO = 32
+# A GPU-box command is killed above ~270 GiB of host memory (the pool's
+# per-command cap, not visible to the process): the reference's footprint is
+# planned below this, and below 0.8 x MemAvailable and any cgroup limit
+HOST_CMD_CAP = 256 << 30
+BENCH_PROC_RESERVE = 8 << 30  # this process (torch + HIP runtime) beside the reference
 
 
 def _baseline_metric():
@@ -75,6 +83,38 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _physical_cores() -> int | None:
+    """Distinct (physical id, core id) pairs of /proc/cpuinfo."""
+    try:
+        cores, phys = set(), None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    cores.add((phys, line.split(":", 1)[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
+
+
+def _cgroup_cpu_quota() -> float | None:
+    """CPUs' worth of time this cgroup may use (cpu.max), None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
+def _cgroup_mem_limit() -> int | None:
+    try:
+        v = open("/sys/fs/cgroup/memory.max").read().strip()
+        return None if v == "max" else int(v)
+    except (OSError, ValueError):
+        return None
+
+
 def _mem_available() -> int:
     try:
         with open("/proc/meminfo") as f:
@@ -87,8 +127,30 @@ def _mem_available() -> int:
 
 
 def _host() -> dict:
-    return {"cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
-            "mem_available_GiB": round(_mem_available() / 2**30, 1)}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": _cpu_model(), "host_cpus": os.cpu_count(), "physical_cores": _physical_cores(),
+            "cpu_affinity": affinity, "cgroup_cpu_quota": _cgroup_cpu_quota(),
+            "mem_available_GiB": round(_mem_available() / 2**30, 1),
+            "cgroup_mem_limit_GiB": None if _cgroup_mem_limit() is None else round(_cgroup_mem_limit() / 2**30, 1)}
+
+
+def _host_budget() -> int:
+    """Host bytes the reference may touch: 0.8 x MemAvailable, the cgroup
+    limit and the box's per-command cap, less this process's own share."""
+    b = min(int(_mem_available() * 0.8), int(HOST_CMD_CAP * 0.9))
+    lim = _cgroup_mem_limit()
+    if lim is not None:
+        b = min(b, int(lim * 0.9))
+    return b - BENCH_PROC_RESERVE
+
+
+def _child_peak_rss() -> int:
+    """Peak RSS (bytes) of the largest child process that has exited so far."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss * 1024
 
 
 def _run_ref(path: str, n: int, p: int, timeout: int = 900):
@@ -101,30 +163,74 @@ def _run_ref(path: str, n: int, p: int, timeout: int = 900):
     return float(r.stdout.strip().splitlines()[-1].split("\t")[2]), wall
 
 
-def ref_workers(log_n: int, esz: int, threads: int) -> int:
-    """The largest power of two P <= threads whose reference footprint fits:
-    in + out (2 S) plus 2 S of scratch per worker (CPU.c:225-239, 396-407)."""
-    s = (1 << log_n) * esz
-    budget = min(int(_mem_available() * 0.7), CPU_MEM_CAP)
+def _union_len(iv) -> int:
+    tot, end = 0, -1
+    for a, b in sorted(iv):
+        if b <= end:
+            continue
+        tot += b - max(a, end)
+        end = b
+    return tot
+
+
+def ref_touched_elems(n: int, p: int) -> int:
+    """Elements of host memory the reference touches with p workers (-o runs):
+    `in` (written by initialize_data, CPU.c:220-247; `out` stays untouched
+    without -t) and, per worker, all of tmp_in (copy_to, CPU.c:407) plus the
+    tmp_out pages its tree levels and cylinder stages write (CPU.c:419-478,
+    the two scratchpads swapping after every level)."""
+    lp = p.bit_length() - 1
+    m = n // p
+    total = n
+    for q in range(p):
+        written = [[], []]  # ranges written into the original tmp_in / tmp_out
+        cur, size, it = 1, n, lp
+        while size > m:
+            off = (q >> it) * size
+            left = ((q >> (it - 1)) & 1) == 0
+            written[cur].append((off, off + size // 2) if left else (off + size // 2, off + size))
+            cur ^= 1
+            size //= 2
+            it -= 1
+        size = m
+        while size > 1:
+            written[cur].append((q * m, q * m + m))
+            cur ^= 1
+            size //= 2
+        total += n + _union_len(written[1])
+    return total
+
+
+def ref_workers(log_n: int, esz: int, threads: int | None = None) -> int:
+    """The reference's worker count for the CPU baseline: its own sweep's
+    largest p (REF_P_TO = 32, not above the online CPUs as how_many_cores
+    rules, CPU.c:200), halved until the host memory it touches
+    (ref_touched_elems) fits _host_budget()."""
+    cap = threads or min(REF_P_TO, os.cpu_count() or 1)
     p = 1
-    while p * 2 <= threads and (2 + 2 * p * 2) * s <= budget:
+    while p * 2 <= cap:
         p *= 2
-    if (2 + 2 * p) * s > budget:
-        raise RuntimeError(f"N=2^{log_n} needs {(2 + 2 * p) * s / 2**30:.0f} GiB of host memory, "
+    budget = _host_budget()
+    while p > 1 and ref_touched_elems(1 << log_n, p) * esz > budget:
+        p //= 2
+    need = ref_touched_elems(1 << log_n, p) * esz
+    if need > budget:
+        raise RuntimeError(f"N=2^{log_n} needs {need / 2**30:.0f} GiB of host memory, "
                            f"{budget / 2**30:.0f} GiB available")
     return p
 
 
-def cpu_baseline(log_n: int, prec: int, threads: int, workers: int | None = None, repeat: int = 1,
+def cpu_baseline(log_n: int, prec: int, threads: int | None = None, workers: int | None = None, repeat: int = 1,
                  batch: int = 1, slice_of: int = 0) -> dict:
     """The reference CPU path at N = 2^log_n: oracle/_ref (CPU.c built -O2,
-    -Dfloat=double for fp64) with P = `workers` pthreads (default: as many as
-    the threads and host memory allow).  Its own timer (worker 0's tree +
-    cylinder, CPU.c:414-491) gives the time.  repeat > 1 takes the median of
-    that many runs; batch > 1 scales one transform's time to the batch (the
-    reference has no batch: a batch is a loop of run()).  slice_of = P: the
-    time is ONE worker's share of a P-worker split (worker 0's own time),
-    reported as the rate of the whole transform at that time."""
+    -Dfloat=double for fp64) with P = `workers` pthreads (default:
+    ref_workers -- the reference's own p_to = 32 where the host allows).  Its
+    own timer (worker 0's tree + cylinder, CPU.c:414-491) gives the time.
+    repeat > 1 takes the median of that many runs; batch > 1 scales one
+    transform's time to the batch (the reference has no batch: a batch is a
+    loop of run()).  slice_of = P: the time is ONE worker's share of a
+    P-worker split (worker 0's own time), reported as the rate of the whole
+    transform at that time."""
     import pifft_oracle as oracle
     n = 1 << log_n
     esz = 16 if prec == 64 else 8
@@ -153,9 +259,24 @@ def cpu_baseline(log_n: int, prec: int, threads: int, workers: int | None = None
     if slice_of:
         what += f"; one worker's share of the {slice_of}-way split, rated as the whole transform"
     what += f"; process wall {sum(r[1] for r in runs):.1f} s"
-    footprint = (2 + 2 * p) * n * esz
     return {"value": round(flops / (ms * 1e6), 4), "unit": "GFLOP/s", "cores": p, "kind": "reference",
-            "ms": round(ms, 3), "sample": what, "host_bytes": footprint, **_host()}
+            "ms": round(ms, 3), "sample": what, "host_bytes_touched": ref_touched_elems(n, p) * esz,
+            "child_peak_rss_GiB": round(_child_peak_rss() / 2**30, 2), **_host()}
+
+
+def headline_cpu_baseline(log_n: int, prec: int, batch: int = 1, threads: int | None = None) -> dict:
+    """cpu_baseline of a bench line: the reference at the reference's own
+    p_to (32 where the host allows), plus p = 16 beside it at large N (the
+    round-2 baseline), each with its own timer."""
+    cl = log_n
+    rec = cpu_baseline(cl, prec, threads, batch=batch, repeat=1 if cl > 16 else 15)
+    if rec.get("kind") == "reference" and rec["cores"] > 16 and cl > 16:
+        try:
+            alt = cpu_baseline(cl, prec, workers=16, batch=batch)
+            rec["p16"] = {k: alt[k] for k in ("value", "cores", "ms", "sample")}
+        except Exception as e:  # reported, never silently replaced
+            rec["p16"] = {"value": None, "error": repr(e)}
+    return rec
 
 
 def load_traffic(config_key: str, launch_indices):
@@ -215,11 +336,12 @@ class Job:
 
     def run(self, steps, warmup, barrier=lambda: None, profile=True):
         """W untimed steps, then exactly K steps between barrier + synchronize
-        on both sides.  profile: per-launch HIP events recorded on the launch
-        stream inside the timed region (no host syncs; each event record
-        costs ~4 us of GPU time between launches, noise for the 4.6-ms
-        headline step, not for the 10-40 us secondary configs, which time a
-        clean loop and a profiled one).  Returns this rank's seconds."""
+        on both sides.  profile: every launch of the timed steps carries a
+        start and a stop event bound to its own dispatch (pifft_profile_*:
+        hipExtLaunchKernel events, the kernel's start/end timestamps as
+        rocprofv3 reports them; no marker packets, no host syncs), so the
+        per-launch means come from the same loop as the step time and cannot
+        add up to more than it.  Returns this rank's seconds."""
         torch = self.torch
         for _ in range(warmup):
             self.step()
@@ -240,25 +362,37 @@ class Job:
             self.avg = [s / steps for s in sums]
         return elapsed
 
-    def roofline(self) -> dict:
+    def roofline(self, ms_per_step: float) -> dict:
         """The dominant kernel (the kernel function with the largest share of
         the step; its launches grouped as rocprofv3 --stats groups them):
-        algorithmic bytes per launch / its mean launch duration."""
+        algorithmic bytes per launch / its mean launch duration.  Self-check:
+        no frac is emitted when that kernel's time per step (or all launches'
+        time) exceeds the step time of the loop it was measured in."""
         d, avg = self.desc, self.avg
         nl = d["num_launches"]
         by_fn = {}
         for i in range(nl):
             by_fn.setdefault(d["launch_fn"][i], []).append(i)
         dom_launches = max(by_fn.values(), key=lambda ls: sum(avg[i] for i in ls))
-        dom_ms = sum(avg[i] for i in dom_launches) / len(dom_launches)
+        dom_step_ms = sum(avg[i] for i in dom_launches)
+        dom_ms = dom_step_ms / len(dom_launches)
         dom_bytes = sum(d["launch_bytes"][i] for i in dom_launches) // len(dom_launches)
+        kernel_step_ms = sum(avg[:nl])
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        return {"bound": "hbm",
-                "kernel": (f"{d['launch_kind'][dom_launches[0]]} kernel of launches {dom_launches} "
-                           f"(mean launch {dom_ms:.4f} ms, HIP events on the launch stream)"),
-                "launches": dom_launches, "mean_ms": round(dom_ms, 5),
-                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": dom_bytes}
+        rec = {"bound": "hbm",
+               "kernel": (f"{d['launch_kind'][dom_launches[0]]} kernel of launches {dom_launches} "
+                          f"(mean launch {dom_ms:.4f} ms, kernel-bound HIP events on the launch stream)"),
+               "launches": dom_launches, "mean_ms": round(dom_ms, 5),
+               "kernel_name": self.plan.kernel_name(dom_launches[0]),
+               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": dom_bytes,
+               "kernel_ms_per_step": round(dom_step_ms, 6), "all_launches_ms_per_step": round(kernel_step_ms, 6),
+               "step_ms": round(ms_per_step, 6)}
+        if dom_ms <= 0 or dom_step_ms > ms_per_step or kernel_step_ms > ms_per_step:
+            rec.update({"achieved": None, "frac": None,
+                        "error": f"refused: launches take {kernel_step_ms:.6f} ms (dominant {dom_step_ms:.6f} ms) "
+                                 f"per {ms_per_step:.6f}-ms step"})
+        return rec
 
     def launches(self) -> list:
         d, out = self.desc, []
@@ -289,6 +423,8 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
          dict(log_n=20, prec=64, workers=8, repeat=5, slice_of=8)),
         ("C3", "config 3: batched fp32 4096 x N=4096", dict(log_n=12, prec=F32, P=1, first=0, count=1, batch=4096),
          dict(log_n=12, prec=32, workers=1, repeat=31, batch=4096)),
+        ("C4_f32", "config 4 in the reference's own data_t: one fp32 complex N=2^28 transform",
+         dict(log_n=28, prec=F32, P=1, first=0, count=1, batch=1), dict(log_n=28, prec=32)),
     ]
     out = {}
     for key, what, g, c in cases:
@@ -297,17 +433,19 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             n = 1 << g["log_n"]
             job = Job(pifft, torch, gpu, n=n, P=g["P"], prec=g["prec"], first=g["first"], count=g["count"],
                       batch_local=g["batch"], b_first=0, seed=seed)
-            # small steps: more of them, so the timed loop is not launch-jitter;
-            # a clean timed loop for the step time, a profiled one for the roofline
-            k = max(steps, 50)
-            elapsed = job.run(k, max(warmup, 5), profile=False)
-            job.run(k, 2)
+            # small steps: more of them, so the timed loop is not launch-jitter.
+            # The timed loop carries the kernel-bound per-launch events (they
+            # add nothing to the stream); a clean loop beside it shows that
+            k = max(steps, 50) if g["log_n"] < 24 else max(steps, 20)
+            elapsed = job.run(k, max(warmup, 5))
             ms = elapsed * 1e3 / k
+            clean = job.run(k, 2, profile=False) * 1e3 / k
             flops = 5.0 * n * g["log_n"] * g["batch"]
             rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
+                        "clean_ms_per_step": round(clean, 6),
                         "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],
                         "workers_in_plan": g["count"], "batch": g["batch"], "passes": job.desc["num_passes"],
-                        "radix": job.desc["radix"], "launches": job.launches(), "roofline": job.roofline()})
+                        "radix": job.desc["radix"], "launches": job.launches(), "roofline": job.roofline(ms)})
             job.free()
         except Exception as e:  # reported, never silently replaced
             rec["error"] = repr(e)
@@ -320,24 +458,59 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
     return out
 
 
-def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev, log_n=32) -> dict:
+C5_HEADROOM = 4 << 30  # HBM left free beside config 5's largest phase
+
+
+def c5_hbm_need(n: int, world: int, esz: int = 16) -> int:
+    """Config 5's peak HBM per GPU: the timed phase holds the input replica, the
+    slice and the plan's workspace (n + 2 n/world values); the exchange, after
+    the replica and the plan are freed, holds the slice, the gathered buffer
+    and the natural-order result (n/world + 2 n)."""
+    return max(n + 2 * (n // world), n // world + 2 * n) * esz + C5_HEADROOM
+
+
+def all_ranks_ok(ok: bool, dist, red_dev) -> bool:
+    """True only if every rank says ok (one all-reduce, so that all ranks take
+    the same branch and no collective is left waiting on a rank that skipped)."""
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=red_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev, log_n=32,
+            same_device=False) -> dict:
     """Config 5 on a multi-GPU job: fp64 N=2^32 split over `world` GPUs (one
     worker per GPU, 64 GiB input replica each), then the RCCL all-gather and
     interleave into natural order (timed separately).  log_n < 32: a smaller
-    rehearsal of the same code path."""
+    rehearsal of the same code path.  Every rank first checks its free HBM
+    against the config's peak (c5_hbm_need); if any rank is short, all ranks
+    report the error instead of allocating (no out-of-memory mid-collective)."""
     import pifft_dist
     n = 1 << log_n
     rec = {"workload": f"config 5: fp64 N=2^{log_n} over {world} GPUs, one worker each (no data-path collective), "
                        f"then the all-gather ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()}) "
                        f"+ interleave"}
+    torch.cuda.empty_cache()
+    free, total = torch.cuda.mem_get_info(gpu)
+    need = c5_hbm_need(n, world)
+    if same_device:
+        need = need * world  # every rehearsal rank shares one GPU
+    rec["hbm_need_GiB"], rec["hbm_free_GiB"] = round(need / 2**30, 2), round(free / 2**30, 2)
+    if not all_ranks_ok(free >= need, dist, red_dev):
+        rec["error"] = (f"not run: config 5 needs {need / 2**30:.1f} GiB of HBM per GPU and at least one rank has "
+                        f"less free (this rank {free / 2**30:.1f} of {total / 2**30:.1f} GiB)")
+        return rec
     job = Job(pifft, torch, gpu, n=n, P=world, prec=pifft.F64, first=rank, count=1, batch_local=1, b_first=0,
               seed=seed)
-    elapsed = pifft_dist.max_over_ranks(job.run(steps, warmup, barrier), red_dev)
+    local_s = job.run(steps, warmup, barrier)
+    elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms = elapsed * 1e3 / steps
     rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
                 "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(),
-                "roofline_rank0": job.roofline() if rank == 0 else None})
+                "roofline_rank0": job.roofline(local_s * 1e3 / steps) if rank == 0 else None})
     job.x = None  # the 64 GiB replica is not needed by the exchange
+    job.plan.close()  # nor the plan's workspace
     torch.cuda.empty_cache()
     rec["allgather_ms"] = round(allgather(pifft, torch, dist, job, barrier, red_dev), 3)
     job.free()
@@ -348,7 +521,8 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
     """Configs 2 and 3 on a multi-GPU job, each a timed loop with the headline's
     barrier + max-over-ranks contract: C2 split one worker per GPU (the
     reference's 8-way split on real GPUs, P = world), C3's 4096 transforms
-    sharded by transform over the GPUs."""
+    sharded by transform over the GPUs.  Rank 0's dominant-kernel roofline
+    comes from the same loop."""
     import pifft_dist
     F64, F32 = pifft.F64, pifft.F32
     b0, bc = pifft_dist.batch_range(rank, world, 4096)
@@ -364,11 +538,13 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
         try:
             job = Job(pifft, torch, gpu, n=1 << log_n, prec=prec, seed=seed, **g)
             k = max(steps, 50)
-            elapsed = pifft_dist.max_over_ranks(job.run(k, max(warmup, 5), barrier, profile=False), red_dev)
+            local_s = job.run(k, max(warmup, 5), barrier)
+            elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
             ms = elapsed * 1e3 / k
             rec.update({"value": round(5.0 * (1 << log_n) * log_n * batch / (ms * 1e-3) / 1e9, 2),
                         "unit": "GFLOP/s", "ms_per_step": round(ms, 6), "steps": k, "n_gpus": world,
-                        "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"]})
+                        "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"],
+                        "roofline_rank0": job.roofline(local_s * 1e3 / k) if rank == 0 else None})
             job.free()
         except Exception as e:  # reported, never silently replaced
             rec["error"] = repr(e)
@@ -377,20 +553,28 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
 
 
 def allgather(pifft, torch, dist, job, barrier, red_dev) -> float:
-    """The optional final exchange: RCCL all-gather of every rank's slices,
-    then the stride-P interleave into natural order on every GPU (ms, max over
-    ranks)."""
+    """The optional final exchange: RCCL all-gather of every rank's result,
+    then -- for a worker split -- the stride-P interleave into natural order on
+    every GPU (ms, max over ranks).  A batch-sharded job (every plan holds all
+    P workers, count == P) gathers whole transforms already in natural order:
+    no interleave.  With several transforms per rank the gathered buffer is
+    rank-major (rank, transform, slices) and is reordered to the
+    transform-major slice layout the interleave reads."""
     import pifft_dist
     torch.cuda.synchronize(job.dev)
     barrier()
     ta = time.perf_counter()
     gathered = pifft_dist.allgather_slices(job.y)
-    natural = torch.empty(job.n * job.batch_local, dtype=job.y.dtype, device=job.dev)
-    pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), job.n, job.P, job.batch_local, job.prec,
-                            job.stream)
+    if job.count < job.P:
+        world = gathered.numel() // job.y.numel()
+        batch = job.batch_local
+        gathered = pifft_dist.slices_transform_major(gathered, world, batch)
+        natural = torch.empty(job.n * batch, dtype=job.y.dtype, device=job.dev)
+        pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), job.n, job.P, batch, job.prec, job.stream)
+        del natural
     torch.cuda.synchronize(job.dev)
     ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
-    del gathered, natural
+    del gathered
     return ms
 
 
@@ -417,7 +601,9 @@ def main() -> int:
                     help="config 5 size at 8 GPUs (default 2^32; smaller only to rehearse the code path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-log-n", type=int, default=0, help="CPU baseline size (default: the headline N)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="reference pthreads for the CPU baseline (default: the reference's own p_to = 32, "
+                         "within the online CPUs and host memory)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (use with --dist-backend gloo)")
@@ -456,11 +642,15 @@ def main() -> int:
     dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
+        # fail fast: a stuck collective on a first multi-GPU run ends in 3 min,
+        # not at the default watchdog
+        tmo = datetime.timedelta(seconds=int(os.environ.get("BENCH_DIST_TIMEOUT_S", "180")))
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=tmo)
 
     def barrier():
         if dist is not None:
@@ -487,7 +677,10 @@ def main() -> int:
     local_s = job.run(args.steps, args.warmup, barrier)
     elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms_per_step = elapsed * 1e3 / args.steps
-    rf = job.roofline()
+    rf = job.roofline(local_s * 1e3 / args.steps)
+    # the same steps without the per-launch events (evidence that the
+    # kernel-bound events add nothing to the timed loop)
+    clean_ms = pifft_dist.max_over_ranks(job.run(args.steps, 1, barrier, profile=False), red_dev) * 1e3 / args.steps
     desc = job.desc
     launches = job.launches()
     config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
@@ -517,7 +710,8 @@ def main() -> int:
             if world == 8 and (not args.same_device or args.c5_log_n < 32):
                 try:
                     secondary["C5"] = config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
-                                              min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n)
+                                              min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n,
+                                              same_device=args.same_device)
                 except Exception as e:  # reported, never silently replaced
                     secondary["C5"] = {"error": repr(e)}
 
@@ -526,7 +720,11 @@ def main() -> int:
     value = flops / (ms_per_step * 1e-3) / 1e9
     if rank == 0:
         rf_line = {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac")}
-        rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"]})
+        rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"],
+                        "kernel_ms_per_step": rf["kernel_ms_per_step"],
+                        "all_launches_ms_per_step": rf["all_launches_ms_per_step"], "step_ms": rf["step_ms"]})
+        if "error" in rf:
+            rf_line["error"] = rf["error"]
         line = {
             "metric": _baseline_metric(),
             "value": round(value, 2),
@@ -555,6 +753,7 @@ def main() -> int:
                 "lines_per_workgroup": desc["lines"],
                 "hbm_bytes_per_step_algorithmic": total_bytes,
                 "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                "clean_ms_per_step": round(clean_ms, 6),
                 "launches": launches,
                 "parallelism": (f"batch-split {args.batch}/{world} per GPU, p{P}" if args.shard == "batch" else
                                 f"pi-split p{P} over {world} GPU(s)"),
@@ -566,15 +765,12 @@ def main() -> int:
             "roofline": rf_line,
             "cpu_baseline": None,
         }
-        if world == 1 and not emulated and not args.no_cpu_baseline:
-            threads = args.cpu_threads
-            ncpu = os.cpu_count() or 1
-            while threads > ncpu:
-                threads //= 2
+        # rank 0 of every job (also N > 1, so the driver's scaling lines carry
+        # it), after the GPU work: the other ranks do not wait for it
+        if not emulated and not args.no_cpu_baseline:
             try:
-                cl = args.cpu_log_n or args.log_n
-                line["cpu_baseline"] = cpu_baseline(cl, args.prec, max(1, threads), batch=args.batch,
-                                                    repeat=1 if cl > 16 else 15)
+                line["cpu_baseline"] = headline_cpu_baseline(args.cpu_log_n or args.log_n, args.prec,
+                                                             batch=args.batch, threads=args.cpu_threads or None)
             except Exception as e:  # reported, never silently replaced
                 line["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(line), flush=True)

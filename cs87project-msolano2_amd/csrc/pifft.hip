@@ -20,6 +20,7 @@
 #include "pifft_table.h"
 #include "../../include/pifft.h"
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -27,6 +28,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <cxxabi.h>
 
 #include <algorithm>
 #include <string>
@@ -149,7 +152,7 @@ struct pifft_plan {
     int tree_steps = 0, npasses = 0;
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
     std::vector<Step> tree_only;  // the tree stage alone, for pifft_tree_device
-    std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: steps x (launches + 1)
+    std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: steps x 2 launches (start, stop of each)
     int prof_steps = 0, prof_used = 0;
     int radix[8] = {0}, lines[8] = {0}, vpt[8] = {0};
     void* buf[NBUF] = {nullptr};
@@ -158,7 +161,7 @@ struct pifft_plan {
     void* d_tw = nullptr;
     size_t tw_bytes = 0;
     hipStream_t stream = nullptr;
-    std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t> ev;  // 2 per launch: its start and stop (launch_steps)
     void* d_hin = nullptr;   // pifft_execute's staging copies
     void* d_hout = nullptr;
     void* d_gather = nullptr;  // pifft_allgather: every worker's slices on this plan's device
@@ -843,7 +846,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
     if (p->bytes_ch) HIPCHK(hipMalloc(&p->buf[BUF_CH], p->bytes_ch));
     HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    p->ev.resize(p->steps.size() + 1);
+    p->ev.resize(2 * p->steps.size());
     for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
     return 0;
 }
@@ -896,10 +899,21 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
     return 0;
 }
 
-int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hipStream_t st) {
+// One launch.  With events (e0, e1): hipExtLaunchKernel binds them to the
+// kernel's own dispatch (its start and end timestamps, what rocprofv3 reports
+// as the kernel's duration) -- no marker packet between launches.  Marker
+// events (hipEventRecord before every launch) cost ~4 us of GPU time each and
+// made the per-launch means of the 10-50 us configs longer than their steps
+// (round-2 verdict); kernel-bound events add nothing to the stream.
+int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hipStream_t st,
+                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     void* base[NBUF] = {const_cast<void*>(d_in), d_out, p->buf[BUF_W], p->buf[BUF_TA], p->buf[BUF_TB], p->buf[BUF_CH]};
     const char* src = (const char*)base[s.src] + s.src_off * p->esz;
     char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
+    auto go = [&](void** args, size_t lds) {
+        return e0 ? hipExtLaunchKernel(s.fn, s.grid, s.block, args, lds, st, e0, e1, 0)
+                  : hipLaunchKernel(s.fn, s.grid, s.block, args, lds, st);
+    };
     hipError_t e = hipSuccess;
     switch (s.kind) {
         case STEP_PASS:
@@ -910,7 +924,7 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             a.in = src;
             a.out = dst;
             void* args[] = {&a};
-            e = hipLaunchKernel(s.fn, s.grid, s.block, args, s.lds, st);
+            e = go(args, s.lds);
             break;
         }
         case STEP_TREE: {
@@ -918,7 +932,7 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             a.in = src;
             a.out = dst;
             void* args[] = {&a};
-            e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
+            e = go(args, 0);
             break;
         }
         case STEP_INTERLEAVE: {
@@ -927,13 +941,30 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             uint64_t total = s.il_total;
             uint32_t ln = s.il_log_n, lpp = s.il_log_p;
             void* args[] = {&in, &o, &total, &ln, &lpp};
-            e = hipLaunchKernel(s.fn, s.grid, s.block, args, 0, st);
+            e = go(args, 0);
             break;
         }
         default:
             return fail("bad step kind %d", s.kind);
     }
     if (e != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// every launch of the plan; ev (or NULL): 2 events per launch, its start and stop
+int launch_steps(pifft_plan* p, const void* d_in, void* d_out, hipStream_t st, hipEvent_t* ev) {
+    for (size_t i = 0; i < p->steps.size(); i++)
+        if (launch_step(p, p->steps[i], d_in, d_out, st, ev ? ev[2 * i] : nullptr, ev ? ev[2 * i + 1] : nullptr))
+            return -1;
+    return 0;
+}
+
+// per-launch durations of one recorded execution (ev as launch_steps)
+int read_launch_ms(size_t ns, hipEvent_t* ev, std::vector<float>& ms) {
+    ms.assign(ns, 0.0f);
+    if (!ns) return 0;
+    HIPCHK(hipEventSynchronize(ev[2 * ns - 1]));
+    for (size_t i = 0; i < ns; i++) HIPCHK(hipEventElapsedTime(&ms[i], ev[2 * i], ev[2 * i + 1]));
     return 0;
 }
 
@@ -946,18 +977,10 @@ int check_buffers(const pifft_plan* p, const void* d_in, void* d_out) {
 
 uint64_t out_elems(const pifft_plan* p) { return (uint64_t)p->batch * p->nq * p->m; }
 
-// run every step with an event before each launch and after the last
+// run every step with kernel-bound events, wait, per-launch durations
 int run_timed(pifft_plan* p, const void* d_in, void* d_out, hipStream_t st, std::vector<float>& ms) {
-    const size_t ns = p->steps.size();
-    for (size_t i = 0; i < ns; i++) {
-        HIPCHK(hipEventRecord(p->ev[i], st));
-        if (launch_step(p, p->steps[i], d_in, d_out, st)) return -1;
-    }
-    HIPCHK(hipEventRecord(p->ev[ns], st));
-    HIPCHK(hipEventSynchronize(p->ev[ns]));
-    ms.assign(ns, 0.0f);
-    for (size_t i = 0; i < ns; i++) HIPCHK(hipEventElapsedTime(&ms[i], p->ev[i], p->ev[i + 1]));
-    return 0;
+    if (launch_steps(p, d_in, d_out, st, p->ev.data())) return -1;
+    return read_launch_ms(p->steps.size(), p->ev.data(), ms);
 }
 
 void stage_split(const pifft_plan* p, const std::vector<float>& ms, double* s1, double* s2) {
@@ -1196,25 +1219,32 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     return 0;
 }
 
+int pifft_plan_kernel_name(const pifft_plan* p, int launch, char* buf, size_t len) {
+    if (!p || !buf || len == 0) return fail("NULL argument");
+    if (launch < 0 || launch >= (int)p->steps.size()) return fail("launch %d out of range", launch);
+    DeviceGuard g(p->device);
+    const char* mangled = hipKernelNameRefByPtr(p->steps[(size_t)launch].fn, nullptr);
+    if (!mangled) return fail("no kernel name for launch %d", launch);
+    int st = 0;
+    char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+    snprintf(buf, len, "%s", (st == 0 && dem) ? dem : mangled);
+    free(dem);
+    return 0;
+}
+
 int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* stream) {
     if (check_buffers(p, d_in, d_out)) return -1;
     DeviceGuard g(p->device);
     hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
-    const size_t ns = p->steps.size();
     hipEvent_t* ev = nullptr;
-    if (p->prof_used < p->prof_steps) ev = &p->prof_ev[(size_t)p->prof_used++ * (ns + 1)];
-    for (size_t i = 0; i < ns; i++) {
-        if (ev) HIPCHK(hipEventRecord(ev[i], st));
-        if (launch_step(p, p->steps[i], d_in, d_out, st)) return -1;
-    }
-    if (ev) HIPCHK(hipEventRecord(ev[ns], st));
-    return 0;
+    if (p->prof_used < p->prof_steps) ev = &p->prof_ev[(size_t)p->prof_used++ * 2 * p->steps.size()];
+    return launch_steps(p, d_in, d_out, st, ev);
 }
 
 int pifft_profile_start(pifft_plan* p, int steps) {
     if (!p || steps < 0) return fail("bad arguments");
     DeviceGuard g(p->device);
-    const size_t need = (size_t)steps * (p->steps.size() + 1);
+    const size_t need = (size_t)steps * 2 * p->steps.size();
     while (p->prof_ev.size() < need) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -1231,16 +1261,11 @@ int pifft_profile_read(pifft_plan* p, float* launch_ms_sum, int max_launches) {
     const size_t ns = p->steps.size();
     const int used = p->prof_used;
     p->prof_steps = p->prof_used = 0;  // profiling stops, also on an error below
-    std::vector<float> sum(ns, 0.0f);
+    std::vector<float> sum(ns, 0.0f), ms;
     for (int k = 0; k < used; k++) {
-        hipEvent_t* ev = &p->prof_ev[(size_t)k * (ns + 1)];
-        // each execution's end event: the executions may have run on different streams
-        HIPCHK(hipEventSynchronize(ev[ns]));
-        for (size_t i = 0; i < ns; i++) {
-            float ms = 0.0f;
-            HIPCHK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
-            sum[i] += ms;
-        }
+        // each execution's own events: the executions may have run on different streams
+        if (read_launch_ms(ns, &p->prof_ev[(size_t)k * 2 * ns], ms)) return -1;
+        for (size_t i = 0; i < ns; i++) sum[i] += ms[i];
     }
     if (launch_ms_sum)
         for (int i = 0; i < max_launches && i < (int)ns; i++) launch_ms_sum[i] = sum[i];
@@ -1301,21 +1326,14 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
     for (int i = 0; i < np; i++) {
         pifft_plan* p = plans[i];
         DeviceGuard g(p->device);
-        const size_t ns = p->steps.size();
-        for (size_t s = 0; s < ns; s++) {
-            HIPCHK(hipEventRecord(p->ev[s], p->stream));
-            if (launch_step(p, p->steps[s], p->d_hin, p->d_hout, p->stream)) return -1;
-        }
-        HIPCHK(hipEventRecord(p->ev[ns], p->stream));
+        if (launch_steps(p, p->d_hin, p->d_hout, p->stream, p->ev.data())) return -1;
     }
     double t1 = 0, t2 = 0;
     for (int i = 0; i < np; i++) {
         pifft_plan* p = plans[i];
         DeviceGuard g(p->device);
-        const size_t ns = p->steps.size();
-        HIPCHK(hipEventSynchronize(p->ev[ns]));
-        std::vector<float> ms(ns);
-        for (size_t s = 0; s < ns; s++) HIPCHK(hipEventElapsedTime(&ms[s], p->ev[s], p->ev[s + 1]));
+        std::vector<float> ms;
+        if (read_launch_ms(p->steps.size(), p->ev.data(), ms)) return -1;
         double a, b;
         stage_split(p, ms, &a, &b);
         if (a + b > t1 + t2) {  // the slowest GPU sets the job's time

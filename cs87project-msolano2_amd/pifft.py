@@ -69,6 +69,7 @@ _SIGS = {
     "pifft_plan_dry_run": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.POINTER(PlanInfo)]),
     "pifft_plan_get_info": (ctypes.c_int, [_P, ctypes.POINTER(PlanInfo)]),
+    "pifft_plan_kernel_name": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     "pifft_execute_device": (ctypes.c_int, [_P, _P, _P, _P]),
     "pifft_execute_device_timed": (ctypes.c_int, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_float),
                                                   ctypes.c_int]),
@@ -172,6 +173,12 @@ class Plan:
 
     def describe(self) -> dict:
         return describe_info(self.info)
+
+    def kernel_name(self, launch: int) -> str:
+        """Demangled kernel function of one launch (as rocprofv3 names it)."""
+        buf = ctypes.create_string_buffer(512)
+        _check(lib().pifft_plan_kernel_name(self._h, launch, buf, len(buf)), "pifft_plan_kernel_name")
+        return buf.value.decode()
 
     def execute_device(self, d_in: int, d_out: int, stream=None) -> None:
         _check(lib().pifft_execute_device(self._h, d_in, d_out, _stream(stream)), "pifft_execute_device")

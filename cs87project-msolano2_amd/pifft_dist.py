@@ -68,18 +68,30 @@ def allgather_slices(local, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     src = local.contiguous()
+    shape = (world * src.shape[0],) + tuple(src.shape[1:]) if src.dim() else (world,)
     if dist.get_backend(group) == "nccl":
         flat = torch.view_as_real(src).reshape(-1) if src.is_complex() else src.reshape(-1)
         out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
         dist.all_gather_into_tensor(out, flat, group=group)
-        return torch.view_as_complex(out.view(-1, 2)) if src.is_complex() else out
+        out = torch.view_as_complex(out.view(-1, 2)) if src.is_complex() else out
+        return out.view(shape)  # the shape torch.cat of the per-rank parts has (the gloo path)
     staged = src.is_cuda  # gloo gathers host tensors
     if staged:
         src = src.cpu()
     parts = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(parts, src, group=group)
-    out = torch.cat(parts)
+    out = torch.cat(parts) if src.dim() else torch.stack(parts)
     return out.to(local.device) if staged else out
+
+
+def slices_transform_major(gathered, world: int, batch: int):
+    """A worker split's all-gathered result is rank-major -- (rank, transform,
+    that rank's slices) -- while the stride-P interleave reads each transform's
+    P slices back to back (transform, worker, bin).  Reorders the flat
+    gathered buffer (a no-op view for one transform per rank)."""
+    if batch == 1:
+        return gathered.reshape(-1)
+    return gathered.reshape(world, batch, -1).transpose(0, 1).contiguous().reshape(-1)
 
 
 def max_over_ranks(value: float, device=None) -> float:

@@ -121,6 +121,12 @@ int pifft_plan_dry_run(uint64_t n, uint32_t workers, uint32_t first, uint32_t co
 
 int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
 
+/* The kernel function of launch `launch` (< info.num_launches), demangled as
+ * profilers print it (e.g. "void pifft::k_pass<double, 512, 16, 2, 1, 0, 16>
+ * (pifft::PassArgs)"), into buf (len bytes, truncated, NUL-terminated): maps a
+ * plan's launches onto rocprofv3 --stats rows. */
+int pifft_plan_kernel_name(const pifft_plan* plan, int launch, char* buf, size_t len);
+
 /* Device boundary: d_in holds info.in_elems complex values, d_out receives
  * info.out_elems (d_in != d_out; neither is freed).  Asynchronous on `stream`
  * (a hipStream_t; NULL = the default stream, as in other ROCm libraries).
@@ -130,15 +136,18 @@ int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
  * worker its own scratch, CPU.c:396-404). */
 int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* stream);
 
-/* As pifft_execute_device, but records a HIP event before every launch and
- * after the last one on `stream`, waits, and returns each launch's duration in
- * launch_ms[0 .. min(info.num_launches, max_launches)). */
+/* As pifft_execute_device, but times every launch, waits, and returns each
+ * launch's duration in launch_ms[0 .. min(info.num_launches, max_launches)).
+ * The events are bound to the kernels' own dispatches (hipExtLaunchKernel
+ * start/stop events: the kernel's start and end timestamps, what rocprofv3
+ * reports), so timing adds no marker packets between launches. */
 int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, void* stream,
                                float* launch_ms, int max_launches);
 
 /* Asynchronous per-launch timing: after pifft_profile_start(plan, steps),
- * each of the next `steps` pifft_execute_device calls records a HIP event
- * before every launch and after the last one on its stream (no host sync);
+ * each of the next `steps` pifft_execute_device calls binds a start and a stop
+ * event to every launch (kernel-bound, as pifft_execute_device_timed; no host
+ * sync, nothing added to the stream);
  * pifft_profile_read waits for every recorded execution's last event, writes
  * the per-launch duration summed over the recorded executions to
  * launch_ms_sum[0 .. min(num_launches, max_launches)), stops profiling (also

@@ -37,9 +37,20 @@ def _common(d, steps, warmup, n_gpus=1):
     assert abs(d["value"] - flops / (d["ms_per_step"] * 1e-3) / 1e9) <= tol
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    _roofline_ok(rf, d["ms_per_step"] if n_gpus == 1 else None)
+    assert len(d["config"]["launches"]) >= 1
+
+
+def _roofline_ok(rf, ms_per_step=None):
+    """A roofline object is self-consistent: frac = achieved / peak, and the
+    dominant kernel's (and all launches') time per step fits in the step of the
+    loop it was measured in (kernel-bound events; bench.py refuses otherwise)."""
+    assert "error" not in rf, rf
     assert 0 < rf["achieved"] and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["algorithmic_bytes"] > 0
-    assert len(d["config"]["launches"]) >= 1
+    assert 0 < rf["kernel_ms_per_step"] <= rf["all_launches_ms_per_step"] <= rf["step_ms"]
+    if ms_per_step is not None:
+        assert abs(rf["step_ms"] - ms_per_step) <= 1e-5 * ms_per_step + 1e-6
 
 
 def test_bench_default_contract_small():
@@ -62,14 +73,17 @@ def test_bench_gpus_2_spawns_two_ranks():
     """--gpus 2 without torchrun launches two rank processes (rehearsed on one
     GPU with gloo): n_gpus 2, one record per rank, the all-gather timed."""
     d = _bench("--gpus", "2", "--same-device", "--dist-backend", "gloo", "--log-n", "20", "--steps", "3",
-               "--warmup", "1")
+               "--warmup", "1", "--cpu-log-n", "16", "--cpu-threads", "2")
     _common(d, 3, 1, n_gpus=2)
     pr = d["config"]["per_rank"]
     assert [r["rank"] for r in pr] == [0, 1] and [r["workers"] for r in pr] == [[0, 1], [1, 2]]
     assert all(r["ms_per_step"] > 0 and 0 < r["frac"] for r in pr)
     # the job time is the slowest rank's
     assert d["ms_per_step"] >= max(r["ms_per_step"] for r in pr) * 0.999
-    assert d["config"]["allgather_ms"] > 0 and d["cpu_baseline"] is None
+    assert d["config"]["allgather_ms"] > 0
+    # rank 0 carries the reference CPU baseline at N > 1 too (the driver's scaling lines)
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] == "reference"
     # configs 2 (one worker per GPU) and 3 (batch-sharded) as multi-GPU loops
     sec = d["config"]["secondary"]
     assert set(sec) == {"C2_split", "C3_batch"}
@@ -84,7 +98,7 @@ def test_bench_gpus_8_rehearsal_config5():
     gloo ranks on one GPU and a small config 5: the headline, configs 2/3 split
     over the ranks, config 5 and its all-gather all report without error."""
     d = _bench("--gpus", "8", "--same-device", "--dist-backend", "gloo", "--log-n", "20", "--steps", "2",
-               "--warmup", "1", "--c5-log-n", "22")
+               "--warmup", "1", "--c5-log-n", "22", "--no-cpu-baseline")
     _common(d, 2, 1, n_gpus=8)
     assert len(d["config"]["per_rank"]) == 8 and d["config"]["allgather_ms"] > 0
     sec = d["config"]["secondary"]
@@ -93,6 +107,20 @@ def test_bench_gpus_8_rehearsal_config5():
         assert "error" not in rec, (key, rec)
         assert rec["value"] > 0
     assert sec["C5"]["allgather_ms"] > 0 and sec["C3_batch"]["batch_per_gpu"] == 512
+    assert sec["C5"]["hbm_free_GiB"] >= sec["C5"]["hbm_need_GiB"]
+    for key in ("C2_split", "C3_batch"):
+        _roofline_ok(sec[key]["roofline_rank0"])
+    _roofline_ok(sec["C5"]["roofline_rank0"])
+
+
+def test_bench_config5_hbm_check_refuses_cleanly():
+    """Config 5 checks every rank's free HBM against its peak before allocating:
+    a size that cannot fit (2^34 fp64, 8 ranks on one GPU) is reported as an
+    error by all ranks -- no out-of-memory mid-collective, no hang."""
+    d = _bench("--gpus", "8", "--same-device", "--dist-backend", "gloo", "--log-n", "16", "--steps", "2",
+               "--warmup", "1", "--c5-log-n", "34", "--no-cpu-baseline")
+    c5 = d["config"]["secondary"]["C5"]
+    assert "error" in c5 and "not run" in c5["error"] and c5["hbm_need_GiB"] > c5["hbm_free_GiB"]
 
 
 def test_bench_secondary_configs():
@@ -101,11 +129,13 @@ def test_bench_secondary_configs():
     d = _bench("--steps", "2", "--warmup", "1", "--no-cpu-baseline")
     _common(d, 2, 1)
     sec = d["config"]["secondary"]
-    assert set(sec) == {"C1", "C2", "C2_slice", "C3"}
+    assert set(sec) == {"C1", "C2", "C2_slice", "C3", "C4_f32"}
     for key, rec in sec.items():
         assert "error" not in rec, (key, rec)
         flops = 5.0 * rec["n"] * (rec["n"].bit_length() - 1) * rec["batch"]
         assert abs(rec["value"] - flops / (rec["ms_per_step"] * 1e-3) / 1e9) <= rec["value"] * 1e-3 + 0.01
-        assert 0 < rec["roofline"]["frac"] < 1.2
+        _roofline_ok(rec["roofline"], rec["ms_per_step"])
+        assert 0 < rec["roofline"]["frac"] < 1.0
+    assert sec["C4_f32"]["dtype"] == "f32" and sec["C4_f32"]["n"] == 1 << 28
     assert sec["C3"]["dtype"] == "f32" and sec["C3"]["batch"] == 4096
     assert sec["C2"]["workers"] == 8 and sec["C2_slice"]["workers_in_plan"] == 1

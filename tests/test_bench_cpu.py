@@ -32,19 +32,56 @@ def test_as_rank_is_single_process():
     assert r.returncode != 0 and "--as-rank" in r.stderr
 
 
-@pytest.mark.parametrize("avail_gib,threads,log_n,esz,want", [
-    (1024, 16, 28, 16, 16),   # (2 + 32) * 4 GiB = 136 GiB <= the 160 GiB cap
-    (1024, 64, 28, 16, 16),   # 32 workers would need 264 GiB: capped
-    (100, 16, 28, 16, 4),     # 70 GiB budget: (2 + 8) * 4 = 40 GiB fits, P=8 needs 72
-    (64, 8, 20, 16, 8),       # small N: the thread count decides
-    (1024, 1, 20, 16, 1),
+def test_reference_touched_memory_model():
+    """The reference's touched host memory (in + per worker tmp_in + the tmp_out
+    pages its levels write, CPU.c:220-247, 396-478): 3 S at p = 1, and 49 S
+    (196 GiB at fp64 2^28) at the reference's p_to = 32."""
+    n = 1 << 28
+    assert bench.ref_touched_elems(n, 1) == 3 * n
+    assert bench.ref_touched_elems(n, 32) == 49 * n
+    vals = [bench.ref_touched_elems(1 << 12, 1 << k) for k in range(6)]
+    assert vals == sorted(vals)
+
+
+@pytest.mark.parametrize("avail_gib,cpus,threads,log_n,esz,want", [
+    (2900, 256, None, 28, 16, 32),  # the GPU box: p_to = 32 (196 GiB) under the per-command cap
+    (2900, 256, 16, 28, 16, 16),    # --cpu-threads 16
+    (100, 256, None, 28, 16, 8),    # 72 GiB budget: p = 8 touches 52 GiB, p = 16 100 GiB
+    (2900, 8, None, 28, 16, 8),     # 8 online CPUs: how_many_cores caps p (CPU.c:200)
+    (64, 8, 8, 20, 16, 8),          # small N: the thread count decides
+    (1024, 256, 1, 20, 16, 1),
 ])
-def test_reference_worker_count_fits_memory(monkeypatch, avail_gib, threads, log_n, esz, want):
+def test_reference_worker_count(monkeypatch, avail_gib, cpus, threads, log_n, esz, want):
     monkeypatch.setattr(bench, "_mem_available", lambda: avail_gib << 30)
+    monkeypatch.setattr(bench, "_cgroup_mem_limit", lambda: None)
+    monkeypatch.setattr(bench.os, "cpu_count", lambda: cpus)
     assert bench.ref_workers(log_n, esz, threads) == want
+
+
+def test_reference_worker_count_follows_cgroup_limit(monkeypatch):
+    monkeypatch.setattr(bench, "_mem_available", lambda: 2900 << 30)
+    monkeypatch.setattr(bench, "_cgroup_mem_limit", lambda: 110 << 30)  # 91 GiB budget: p = 16 touches 100
+    monkeypatch.setattr(bench.os, "cpu_count", lambda: 256)
+    assert bench.ref_workers(28, 16) == 8
 
 
 def test_reference_worker_count_refuses_oversize(monkeypatch):
     monkeypatch.setattr(bench, "_mem_available", lambda: 16 << 30)
+    monkeypatch.setattr(bench, "_cgroup_mem_limit", lambda: None)
     with pytest.raises(RuntimeError, match="host memory"):
-        bench.ref_workers(28, 16, 16)  # even P=1 needs 16 GiB
+        bench.ref_workers(28, 16, 16)  # even P=1 touches 12 GiB > 4.8 GiB
+
+
+def test_headline_cpu_baseline_runs_the_reference():
+    """The cpu_baseline object a bench line carries (every N, rank 0): the
+    reference binary built from its source, its own timer, the threads used
+    and the host's CPU/memory description."""
+    import pifft_oracle
+    if pifft_oracle.reference_binary(64) is None:
+        pytest.skip("oracle/_ref not built (make -C oracle ref)")
+    rec = bench.headline_cpu_baseline(14, 64, threads=2)
+    assert rec["kind"] == "reference" and rec["cores"] == 2 and rec["value"] > 0 and rec["unit"] == "GFLOP/s"
+    for k in ("host_cpus", "physical_cores", "cpu_affinity", "mem_available_GiB", "host_bytes_touched",
+              "child_peak_rss_GiB"):
+        assert k in rec, k
+    assert "p=2 pthreads" in rec["sample"]

@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, n, P, q_out):
+def _rank_main(rank, world, port, n, P, q_out, batch=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
@@ -35,28 +35,33 @@ def _rank_main(rank, world, port, n, P, q_out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        x = oracle.generate(n, np.complex128)
+        xs = oracle.generate(n, np.complex128, count=batch * n).reshape(batch, n)
         first, count = pifft_dist.worker_range(rank, world, P)
-        mine = np.stack([pifft_dist.slice_of_natural(oracle.worker_bins(x, P, q), P, q)
-                         for q in range(first, first + count)])
+        # this rank's result as a slice-major plan writes it: (transform, its workers, bins)
+        mine = np.stack([np.stack([pifft_dist.slice_of_natural(oracle.worker_bins(xs[b], P, q), P, q)
+                                   for q in range(first, first + count)]) for b in range(batch)])
         local = torch.from_numpy(mine.reshape(-1).view(np.float64).copy())
-        gathered = pifft_dist.allgather_slices(local).numpy().view(np.complex128).reshape(P, n // P)
-        natural = pifft_dist.interleave_slices(gathered)
+        gathered = pifft_dist.allgather_slices(local)
+        gathered = pifft_dist.slices_transform_major(gathered, world, batch).numpy().view(np.complex128)
+        natural = np.stack([pifft_dist.interleave_slices(s.reshape(P, n // P))
+                            for s in gathered.reshape(batch, n)])
         t = pifft_dist.max_over_ranks(float(rank + 1))
         if rank == 0:
-            want = oracle.fft(x, P=1)
+            want = np.stack([oracle.fft(xs[b], P=1) for b in range(batch)])
             q_out.put((natural.tobytes() == want.tobytes(), t))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,P", [(4096, 4), (1 << 14, 8), (256, 2)])
-def test_two_rank_split_gather_equals_transform(n, P):
+@pytest.mark.parametrize("n,P,batch", [(4096, 4, 1), (1 << 14, 8, 1), (256, 2, 1), (1024, 4, 3), (512, 2, 2)])
+def test_two_rank_split_gather_equals_transform(n, P, batch):
+    """batch > 1: the gathered buffer is rank-major and is reordered to the
+    transform-major slice layout before the interleave (bench.py allgather)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, P, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, P, q, batch)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
