@@ -26,14 +26,18 @@ is reported as config.allgather_ms (never part of value; --no-allgather skips
 it).  Every rank's own time and dominant-kernel roofline go to config.per_rank.
 
 Adds to the JSON line:
-  roofline     : the dominant kernel's algorithmic bytes / its mean duration
-                 (HIP events on the launch stream, inside the timed region),
-                 vs 8 TB/s; traffic = PMC-measured HBM bytes per launch from the
-                 committed rocprofv3 summary (profiles/), else null
+  roofline     : the dominant kernel's algorithmic bytes / its mean duration,
+                 vs 8 TB/s.  The duration: after the timed region, each launch
+                 of the plan replayed K times back to back on the launch stream
+                 with events bound to its first and last dispatch
+                 (pifft_time_launch) -- the in-context duration rocprofv3
+                 reports.  Refused (frac null) if the launches take longer than
+                 the measured step.  traffic = PMC-measured HBM bytes per
+                 launch from the committed rocprofv3 summary (profiles/)
   cpu_baseline : the reference CPU path (oracle/_ref, compiled from the
-                 reference source) at the SAME N, rank 0 at --gpus 1 only, with
-                 the largest power-of-two worker count whose (2 + 2P) S bytes
-                 of scratch (CPU.c:396-407) fit the host's memory
+                 reference source) at the SAME N, rank 0 of every job, with the
+                 reference's own p_to = 32 pthreads where the host's memory
+                 allows (ref_touched_elems), and p = 16 beside it
   secondary    : (--gpus 1, default on) configs 1, 2 (whole and one GPU's
                  slice) and 3 timed in the same run, each with its own
                  dominant-kernel roofline and a reference CPU baseline at the
@@ -334,20 +338,14 @@ class Job:
     def step(self):
         self.plan.execute_device(self.x.data_ptr(), self.y.data_ptr(), self.stream)
 
-    def run(self, steps, warmup, barrier=lambda: None, profile=True):
+    def run(self, steps, warmup, barrier=lambda: None):
         """W untimed steps, then exactly K steps between barrier + synchronize
-        on both sides.  profile: every launch of the timed steps carries a
-        start and a stop event bound to its own dispatch (pifft_profile_*:
-        hipExtLaunchKernel events, the kernel's start/end timestamps as
-        rocprofv3 reports them; no marker packets, no host syncs), so the
-        per-launch means come from the same loop as the step time and cannot
-        add up to more than it.  Returns this rank's seconds."""
+        on both sides; nothing but the plan's launches in the timed region.
+        Returns this rank's seconds."""
         torch = self.torch
         for _ in range(warmup):
             self.step()
         torch.cuda.synchronize(self.dev)
-        if profile:
-            self.plan.profile_start(steps)
         barrier()
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
@@ -355,19 +353,24 @@ class Job:
             self.step()
         torch.cuda.synchronize(self.dev)
         barrier()
-        elapsed = time.perf_counter() - t0
-        if profile:
-            recorded, sums = self.plan.profile_read()
-            assert recorded == steps, recorded
-            self.avg = [s / steps for s in sums]
-        return elapsed
+        return time.perf_counter() - t0
+
+    def time_launches(self, reps: int):
+        """Every launch's in-context duration: the launch replayed `reps` times
+        back to back on the launch stream, with events bound to the first and
+        the last dispatch (pifft_time_launch) -- no marker packet between
+        launches (marker events added ~4 us each; kernels isolated by their own
+        events ran 2-5 % faster than back to back, round-3 trace)."""
+        self.avg = [self.plan.time_launch(i, self.x.data_ptr(), self.y.data_ptr(), self.stream, reps)
+                    for i in range(self.desc["num_launches"])]
+        self.reps = reps
 
     def roofline(self, ms_per_step: float) -> dict:
         """The dominant kernel (the kernel function with the largest share of
         the step; its launches grouped as rocprofv3 --stats groups them):
         algorithmic bytes per launch / its mean launch duration.  Self-check:
         no frac is emitted when that kernel's time per step (or all launches'
-        time) exceeds the step time of the loop it was measured in."""
+        time) exceeds the measured step time."""
         d, avg = self.desc, self.avg
         nl = d["num_launches"]
         by_fn = {}
@@ -381,7 +384,8 @@ class Job:
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         rec = {"bound": "hbm",
                "kernel": (f"{d['launch_kind'][dom_launches[0]]} kernel of launches {dom_launches} "
-                          f"(mean launch {dom_ms:.4f} ms, kernel-bound HIP events on the launch stream)"),
+                          f"(mean launch {dom_ms:.4f} ms: each launch replayed back to back on the launch "
+                          f"stream, events bound to the first and last dispatch)"),
                "launches": dom_launches, "mean_ms": round(dom_ms, 5),
                "kernel_name": self.plan.kernel_name(dom_launches[0]),
                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -433,16 +437,13 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             n = 1 << g["log_n"]
             job = Job(pifft, torch, gpu, n=n, P=g["P"], prec=g["prec"], first=g["first"], count=g["count"],
                       batch_local=g["batch"], b_first=0, seed=seed)
-            # small steps: more of them, so the timed loop is not launch-jitter.
-            # The timed loop carries the kernel-bound per-launch events (they
-            # add nothing to the stream); a clean loop beside it shows that
+            # small steps: more of them, so the timed loop is not launch-jitter
             k = max(steps, 50) if g["log_n"] < 24 else max(steps, 20)
             elapsed = job.run(k, max(warmup, 5))
             ms = elapsed * 1e3 / k
-            clean = job.run(k, 2, profile=False) * 1e3 / k
+            job.time_launches(k)
             flops = 5.0 * n * g["log_n"] * g["batch"]
             rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
-                        "clean_ms_per_step": round(clean, 6),
                         "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],
                         "workers_in_plan": g["count"], "batch": g["batch"], "passes": job.desc["num_passes"],
                         "radix": job.desc["radix"], "launches": job.launches(), "roofline": job.roofline(ms)})
@@ -506,6 +507,7 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
     local_s = job.run(steps, warmup, barrier)
     elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms = elapsed * 1e3 / steps
+    job.time_launches(steps)
     rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
                 "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(),
                 "roofline_rank0": job.roofline(local_s * 1e3 / steps) if rank == 0 else None})
@@ -541,6 +543,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
             local_s = job.run(k, max(warmup, 5), barrier)
             elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
             ms = elapsed * 1e3 / k
+            job.time_launches(k)
             rec.update({"value": round(5.0 * (1 << log_n) * log_n * batch / (ms * 1e-3) / 1e9, 2),
                         "unit": "GFLOP/s", "ms_per_step": round(ms, 6), "steps": k, "n_gpus": world,
                         "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"],
@@ -677,10 +680,8 @@ def main() -> int:
     local_s = job.run(args.steps, args.warmup, barrier)
     elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms_per_step = elapsed * 1e3 / args.steps
+    job.time_launches(args.steps)  # after the timed region: each launch replayed K times
     rf = job.roofline(local_s * 1e3 / args.steps)
-    # the same steps without the per-launch events (evidence that the
-    # kernel-bound events add nothing to the timed loop)
-    clean_ms = pifft_dist.max_over_ranks(job.run(args.steps, 1, barrier, profile=False), red_dev) * 1e3 / args.steps
     desc = job.desc
     launches = job.launches()
     config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
@@ -707,7 +708,7 @@ def main() -> int:
         elif world > 1 and args.shard == "workers":
             secondary = multi_secondary(pifft, torch, dist, gpu, rank, world, args.steps, args.warmup, args.seed,
                                         barrier, red_dev)
-            if world == 8 and (not args.same_device or args.c5_log_n < 32):
+            if world == 8:  # (config5 refuses cleanly when the HBM cannot hold it, e.g. a 1-GPU rehearsal at 2^32)
                 try:
                     secondary["C5"] = config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
                                               min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n,
@@ -719,7 +720,7 @@ def main() -> int:
     flops = 5.0 * n * args.log_n * args.batch  # the whole job's batch (every rank's share)
     value = flops / (ms_per_step * 1e-3) / 1e9
     if rank == 0:
-        rf_line = {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac")}
+        rf_line = {k: rf[k] for k in ("bound", "kernel", "kernel_name", "achieved", "peak", "unit", "frac")}
         rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"],
                         "kernel_ms_per_step": rf["kernel_ms_per_step"],
                         "all_launches_ms_per_step": rf["all_launches_ms_per_step"], "step_ms": rf["step_ms"]})
@@ -753,7 +754,6 @@ def main() -> int:
                 "lines_per_workgroup": desc["lines"],
                 "hbm_bytes_per_step_algorithmic": total_bytes,
                 "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                "clean_ms_per_step": round(clean_ms, 6),
                 "launches": launches,
                 "parallelism": (f"batch-split {args.batch}/{world} per GPU, p{P}" if args.shard == "batch" else
                                 f"pi-split p{P} over {world} GPU(s)"),

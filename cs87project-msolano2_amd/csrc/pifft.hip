@@ -170,6 +170,7 @@ struct pifft_plan {
     std::vector<hipStream_t> gst;  // pifft_allgather: one copy stream per source plan
     std::vector<hipEvent_t> gdone;  // ... and its completion event
     hipEvent_t gev[2] = {nullptr, nullptr};  // gather start / end on `stream`
+    hipEvent_t rep_ev[2] = {nullptr, nullptr};  // pifft_time_launch: first dispatch's start, last one's stop
 };
 
 namespace {
@@ -455,6 +456,8 @@ void release(pifft_plan* p) {
     for (auto st : p->gst) (void)hipStreamDestroy(st);
     for (auto e : p->gdone) (void)hipEventDestroy(e);
     for (auto e : p->gev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : p->rep_ev)
         if (e) (void)hipEventDestroy(e);
     for (auto e : p->ev) (void)hipEventDestroy(e);
     for (auto e : p->prof_ev) (void)hipEventDestroy(e);
@@ -911,8 +914,8 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
     const char* src = (const char*)base[s.src] + s.src_off * p->esz;
     char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
     auto go = [&](void** args, size_t lds) {
-        return e0 ? hipExtLaunchKernel(s.fn, s.grid, s.block, args, lds, st, e0, e1, 0)
-                  : hipLaunchKernel(s.fn, s.grid, s.block, args, lds, st);
+        return (e0 || e1) ? hipExtLaunchKernel(s.fn, s.grid, s.block, args, lds, st, e0, e1, 0)
+                          : hipLaunchKernel(s.fn, s.grid, s.block, args, lds, st);
     };
     hipError_t e = hipSuccess;
     switch (s.kind) {
@@ -1239,6 +1242,26 @@ int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* str
     hipEvent_t* ev = nullptr;
     if (p->prof_used < p->prof_steps) ev = &p->prof_ev[(size_t)p->prof_used++ * 2 * p->steps.size()];
     return launch_steps(p, d_in, d_out, st, ev);
+}
+
+int pifft_time_launch(pifft_plan* p, int launch, const void* d_in, void* d_out, void* stream, int reps,
+                      float* ms_avg) {
+    if (check_buffers(p, d_in, d_out)) return -1;
+    if (launch < 0 || launch >= (int)p->steps.size()) return fail("launch %d out of range", launch);
+    if (reps < 1 || !ms_avg) return fail("bad arguments");
+    DeviceGuard g(p->device);
+    hipStream_t st = (hipStream_t)stream;
+    if (p->rep_ev[0] == nullptr)
+        for (auto& e : p->rep_ev) HIPCHK(hipEventCreate(&e));
+    const Step& s = p->steps[(size_t)launch];
+    for (int r = 0; r < reps; r++)
+        if (launch_step(p, s, d_in, d_out, st, r == 0 ? p->rep_ev[0] : nullptr, r == reps - 1 ? p->rep_ev[1] : nullptr))
+            return -1;
+    HIPCHK(hipEventSynchronize(p->rep_ev[1]));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, p->rep_ev[0], p->rep_ev[1]));
+    *ms_avg = ms / (float)reps;
+    return 0;
 }
 
 int pifft_profile_start(pifft_plan* p, int steps) {

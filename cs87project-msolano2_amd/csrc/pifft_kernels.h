@@ -163,13 +163,15 @@ __device__ __forceinline__ void dft(cx<T>* v) {
 // intermediate stays in the Infinity Cache, see PassArgs)
 constexpr bool nt_loads(int nt) { return nt == 1 || nt == 2; }
 constexpr bool nt_stores(int nt) { return nt == 1 || nt == 3; }
+// (the complex value moves as ONE 8- or 16-byte vector: two scalar nt
+// accesses merged by the compiler left fp32 loads waiting on each other)
+template <typename T>
+using vec2_t = T __attribute__((ext_vector_type(2)));
 template <bool NTS, typename T>
 __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
     if constexpr (NTS && PIFFT_NT_LOADS) {
-        cx<T> r;
-        r.re = __builtin_nontemporal_load(&p->re);
-        r.im = __builtin_nontemporal_load(&p->im);
-        return r;
+        const vec2_t<T> r = __builtin_nontemporal_load(reinterpret_cast<const vec2_t<T>*>(p));
+        return cx<T>{r.x, r.y};
     } else {
         return *p;
     }
@@ -177,8 +179,10 @@ __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
 template <bool NTS, typename T>
 __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
     if constexpr (NTS && PIFFT_NT_STORES) {
-        __builtin_nontemporal_store(v.re, &p->re);
-        __builtin_nontemporal_store(v.im, &p->im);
+        vec2_t<T> r;
+        r.x = v.re;
+        r.y = v.im;
+        __builtin_nontemporal_store(r, reinterpret_cast<vec2_t<T>*>(p));
     } else {
         *p = v;
     }
@@ -680,6 +684,9 @@ constexpr int pre_count() {
     return pre_offset<R, C, BM, VPT, PassShape<R, VPT>::NSTG>();
 }
 
+#ifndef PIFFT_SERIAL_BFLY
+#define PIFFT_SERIAL_BFLY 1
+#endif
 template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, cx<T>* pre, int tid, uint64_t tile) {
     using C2 = cx<T>;
@@ -704,6 +711,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     // MODE 2: the inter-pass twiddle factors depend only on (line, b); their
     // two-level table entries are fetched with the data, not after it (a
     // second dependent round trip per workgroup otherwise)
+    // With several butterflies per thread on the same line (c-fast map, NT a
+    // multiple of C: c does not depend on u) the step factor w^{jm NB} is
+    // shared: fetched once, for u = 0.
+    constexpr bool share_anc = St::cfast && U > 1 && St::NT % C == 0;
     [[maybe_unused]] C2 tw_pre[St::first && BM == 2 ? 4 * U : 1];
     if constexpr (St::first && BM == 2) {
         const C2* tlo = static_cast<const C2*>(a.tw_lo);
@@ -715,8 +726,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t jm = global_line<NTS>(a, (tile * C + c) & lb_mask) & ns_mask;
             const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
-            tw_pre[4 * u + 0] = tlo[e0 & hmask];
-            tw_pre[4 * u + 1] = thi[e0 >> a.tw_h];
+            if (!share_anc || u == 0) {
+                tw_pre[4 * u + 0] = tlo[e0 & hmask];
+                tw_pre[4 * u + 1] = thi[e0 >> a.tw_h];
+            }
             tw_pre[4 * u + 2] = tlo[e1 & hmask];
             tw_pre[4 * u + 3] = thi[e1 >> a.tw_h];
         }
@@ -728,8 +741,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int u = 0; u < U; u++) {
             int c, b;
             St::map(tid, u, c, b);
-            const uint64_t line = tile * C + c;
-            const bool ok = line < a.nlines;
+            // a partial last tile loads the last line again for its idle lanes
+            // (their results are never stored): unconditional loads, no
+            // per-load branch
+            const uint64_t line = tile * C + c < a.nlines ? tile * C + c : a.nlines - 1;
             const uint64_t bt = line >> log_lb, l = line & lb_mask;
             constexpr bool CHUNK = NTS == 2 || NTS == 3;
             const uint64_t j = (CHUNK && a.rd_virt) ? l : global_line<NTS>(a, l);
@@ -761,7 +776,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                         const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << log_lb);
 #pragma unroll
                         for (int m = 0; m < P; m++)
-                            w[g][m] = ok ? ld_stream<nt_loads(NTS)>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
+                            w[g][m] = ld_stream<nt_loads(NTS)>(leaf + ((uint64_t)m << log_m));
                     }
                     static_for<0, G, 1>([&](auto gc) {
                         constexpr int g = decltype(gc)::value;
@@ -776,11 +791,11 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 const C2* row = in + bin * a.in_bstride + j + (uint64_t)b * rs;
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs) : C2{(T)0, (T)0};
+                    v[u * q + k] = ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs);
             } else {
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << les)) : C2{(T)0, (T)0};
+                    v[u * q + k] = ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << les));
             }
         }
     }
@@ -797,17 +812,32 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             }
         });
     }
+    // Several radix-16 butterflies per thread (VPT 32): one after the other,
+    // each with its own twiddles -- a scheduling barrier keeps the compiler
+    // from interleaving their temporaries (two concurrent radix-16 DFTs spill
+    // at the 128-VGPR budget of two workgroups per CU)
+    constexpr bool serial = U > 1 && Sh::Q > 16 && PIFFT_SERIAL_BFLY;
     // ---- twiddles before the butterflies ----
     if constexpr (St::first && BM == 2) {
         // w_{Ns R}^{(j mod Ns) r}, r = b + k NB: the k-dependent factor
         // step^k now, the common factor w^{(j mod Ns) b} after the DFT
+        C2 anc[4];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            C2 anc[4];
-            anc[0] = cmul(tw_pre[4 * u + 1], tw_pre[4 * u + 0]);  // = tw2(lo, hi, h, jm NB)
+            if (!share_anc || u == 0) {
+                const int uu = share_anc ? 0 : u;
+                anc[0] = cmul(tw_pre[4 * uu + 1], tw_pre[4 * uu + 0]);  // = tw2(lo, hi, h, jm NB)
 #pragma unroll
-            for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
+                for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
+            }
             apply_powers<q>(&v[u * q], anc);
+            if constexpr (serial) {
+                dft<q>(&v[u * q]);
+                const C2 base = cmul(tw_pre[4 * u + 3], tw_pre[4 * u + 2]);  // = tw2(lo, hi, h, jm b)
+#pragma unroll
+                for (int k = 0; k < q; k++) v[u * q + k] = cmul(v[u * q + k], base);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
     if constexpr (!St::first) {
@@ -830,9 +860,14 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             apply_powers<q>(&v[u * q], anc);
         }
     }
+    if constexpr (!(St::first && BM == 2 && serial)) {
 #pragma unroll
-    for (int u = 0; u < U; u++) dft<q>(&v[u * q]);
-    if constexpr (St::first && BM == 2) {
+        for (int u = 0; u < U; u++) {
+            dft<q>(&v[u * q]);
+            if constexpr (serial) __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    if constexpr (St::first && BM == 2 && !serial) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const C2 base = cmul(tw_pre[4 * u + 3], tw_pre[4 * u + 2]);  // = tw2(lo, hi, h, jm b)

@@ -83,6 +83,8 @@ _SIGS = {
                                                ctypes.c_int, _P]),
     "pifft_tree_device": (ctypes.c_int, [_P, _P, _P, _P]),
     "pifft_profile_start": (ctypes.c_int, [_P, ctypes.c_int]),
+    "pifft_time_launch": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_float)]),
     "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "pifft_allgather": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_P),
                                        ctypes.POINTER(ctypes.c_double)]),
@@ -189,6 +191,13 @@ class Plan:
         _check(lib().pifft_execute_device_timed(self._h, d_in, d_out, _stream(stream), buf, n),
                "pifft_execute_device_timed")
         return list(buf[:n])
+
+    def time_launch(self, launch: int, d_in: int, d_out: int, stream=None, reps: int = 20) -> float:
+        """Mean in-context duration (ms) of one launch replayed `reps` times back to back."""
+        ms = ctypes.c_float()
+        _check(lib().pifft_time_launch(self._h, launch, d_in, d_out, _stream(stream), reps, ctypes.byref(ms)),
+               "pifft_time_launch")
+        return ms.value
 
     def profile_start(self, steps: int) -> None:
         _check(lib().pifft_profile_start(self._h, steps), "pifft_profile_start")

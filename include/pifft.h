@@ -144,6 +144,17 @@ int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* 
 int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, void* stream,
                                float* launch_ms, int max_launches);
 
+/* In-context duration of one launch (< info.num_launches): the launch alone,
+ * `reps` times back to back on `stream` (the buffers and workspace as an
+ * execution of the plan leaves them), with a start event bound to the first
+ * dispatch and a stop event to the last (hipExtLaunchKernel), so no marker
+ * packet or event isolates the launches; *ms_avg = elapsed / reps.  Kernels
+ * timed one at a time with their own events (pifft_profile_*) run 2-5 %
+ * faster than back to back in a stream, where rocprofv3 and the step time see
+ * them (round-3 trace).  Synchronous. */
+int pifft_time_launch(pifft_plan* plan, int launch, const void* d_in, void* d_out, void* stream, int reps,
+                      float* ms_avg);
+
 /* Asynchronous per-launch timing: after pifft_profile_start(plan, steps),
  * each of the next `steps` pifft_execute_device calls binds a start and a stop
  * event to every launch (kernel-bound, as pifft_execute_device_timed; no host
