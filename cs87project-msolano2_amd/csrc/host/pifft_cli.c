@@ -11,7 +11,7 @@
  *            show_usage, print_input/print_output, verify_results (CPU.c:293-302, 659-705)
  *
  *   pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b batch] [-s seed] [-g gpus]
- *         [-w file] [-r] [-x] [-W warmups] [-l]
+ *         [-w file] [-r] [-u] [-x] [-W warmups] [-l]
  *
  * Output: the reference's 5-column TSV "n p total stage1 stage2" in ms
  * (CPU.c:485-492), once.  stage 1 = tree, stage 2 = local FFT (+ reorder).
@@ -22,7 +22,9 @@
  * -g number of GPUs the P workers are spread over (default 1), -w dump the
  * natural-order output (binary), -r keep the output in the reference's own
  * scratch order (bit-reversed, tmp_in before CPU.c:496-499's scatter; no
- * reorder launch), -x extra columns (GFLOP/s, GB/s),
+ * reorder launch), -u keep the tree its own launch (never fused into the first
+ * pass: stage 1 = the tree alone, as the reference's funnel timer, for the
+ * cost-law fit of analyze-results.R:56), -x extra columns (GFLOP/s, GB/s),
  * -W untimed warm-up runs before the timed one (default 1; code-object load),
  * -l list GPUs (the how-many-* utilities).  -n is parsed as 64-bit.
  */
@@ -56,12 +58,13 @@ typedef struct tr {
     int extra;           /* -x */
     int warmups;         /* -W */
     int bitrev;          /* -r */
+    int separate_tree;   /* -u */
 } tr_t;
 
 static void show_usage(void) {
     print_out("\nusage:\n"
               "  pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b <batch>] [-s <seed>]\n"
-              "        [-g <gpus>] [-w <file>] [-r] [-x] [-W <warmups>] [-l]\n"
+              "        [-g <gpus>] [-w <file>] [-r] [-u] [-x] [-W <warmups>] [-l]\n"
               "\noptions:\n"
               "  -n <n>     power of two input size\n"
               "  -p <p>     power of two number of processors (less than n)\n"
@@ -73,6 +76,7 @@ static void show_usage(void) {
               "  -g <g>     GPUs to spread the p workers over (default 1)\n"
               "  -w <file>  write the output (binary data_t; natural order unless -r)\n"
               "  -r         output in the reference's bit-reversed scratch order\n"
+              "  -u         tree stage as its own launch (stage 1 = the tree alone)\n"
               "  -x         extra columns: GFLOP/s, algorithmic GB/s\n"
               "  -W <w>     untimed warm-up runs (default 1)\n"
               "  -l         list GPUs and exit\n"
@@ -111,7 +115,7 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
     t->batch = 1;
     t->gpus = 1;
     t->warmups = 1;
-    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:rxW:l")) != -1) {
+    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:ruxW:l")) != -1) {
         switch (ret) {
             case 'n':
                 if (parse_u64(optarg, &num) || !(num > 1) || !is_power_of_two_u64(num)) {
@@ -172,6 +176,9 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
                 break;
             case 'r':
                 t->bitrev = 1;
+                break;
+            case 'u':
+                t->separate_tree = 1;
                 break;
             case 'x':
                 t->extra = 1;
@@ -321,11 +328,12 @@ int run(tr_t* t) {
     int rc = -1;
     double s1 = 0, s2 = 0;
     if (initialize_data(t)) goto done;
+    const int sep = t->separate_tree ? PIFFT_SEPARATE_TREE : 0;
     for (uint32_t g = 0; g < G; g++) {
         int r = (G == 1) ? pifft_plan_create_slices(&plans[g], t->N, t->P, 0, t->P, t->batch, t->prec, 0,
-                                                    t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_NATURAL)
+                                                    (t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_NATURAL) | sep)
                          : pifft_plan_create_slices(&plans[g], t->N, t->P, g * per, per, t->batch, t->prec,
-                                                    (int)g, t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_SLICES);
+                                                    (int)g, (t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_SLICES) | sep);
         if (r) {
             stderr_out("(GPU %u): %s\n", g, pifft_last_error());
             goto done;

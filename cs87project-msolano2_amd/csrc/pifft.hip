@@ -16,6 +16,7 @@
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE  // sincos (reference_omega)
 #endif
+#include "pifft_gather.h"
 #include "pifft_kernels.h"
 #include "pifft_table.h"
 #include "../../include/pifft.h"
@@ -148,6 +149,7 @@ struct pifft_plan {
     bool natural = true;
     bool bitrev = false;  // PIFFT_OUT_BITREV
     bool ilv = false;     // the last pass stores natural order itself (PassArgs::ilv_log)
+    bool separate_tree = false;  // PIFFT_SEPARATE_TREE: never fuse the tree into a pass
     std::vector<Step> steps;
     int tree_steps = 0, npasses = 0;
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
@@ -437,6 +439,11 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         }
     }
     if (out.empty()) return fail("no pass decomposition for M=2^%d", logm);
+    // tuning: fp32 strided passes at 32 values per thread (512 threads over
+    // the 16384-value tile, PIFFT_TILE32=16384, two workgroups per CU)
+    if (prec == 32 && env_int("PIFFT_VPT32", 0))
+        for (auto& pc : out)
+            if ((pc.mode == 1 || pc.mode == 2) && find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, 32)) pc.vpt = 32;
     // tuning: lines per workgroup of the last pass (its write side's segment width)
     const int last_c = env_int("PIFFT_LAST_C", 0);
     if (last_c > 0 && out.size() > 1 && find_pass(prec, out.back().R, last_c, out.back().mode, out.back().nts))
@@ -568,7 +575,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // (measured, profiles/r02_fuse_all.log: no consistent win, off by default)
     const uint64_t in_mib = ((uint64_t)p->batch * p->n * esz) >> 20;
     const bool fuse_all = p->nq > 1 && in_mib < (uint64_t)env_int("PIFFT_FUSE_ALL_MAX_MIB", 0);
-    const bool may_fuse = p->P > 1 && (p->nq == 1 || fuse_all) && p->lp <= 4 && env_int("PIFFT_FUSE_TREE", 1);
+    const bool may_fuse = p->P > 1 && (p->nq == 1 || fuse_all) && p->lp <= 4 && !p->separate_tree &&
+                          env_int("PIFFT_FUSE_TREE", 1);
     if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0)) return -1;
     if (p->bitrev && !passes.empty()) {
         // the last pass stores in bit-reversed order: its MODE | 4 twin, at
@@ -865,9 +873,10 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
         return fail("invalid worker range [%u, %u) of %u", first, first + count, workers);
     if (batch == 0) return fail("batch must be >= 1");
     if (prec != PIFFT_F32 && prec != PIFFT_F64) return fail("prec must be PIFFT_F32 or PIFFT_F64");
-    if (flags != PIFFT_OUT_NATURAL && flags != PIFFT_OUT_SLICES && flags != PIFFT_OUT_BITREV)
+    const int order = flags & ~PIFFT_SEPARATE_TREE;
+    if (order != PIFFT_OUT_NATURAL && order != PIFFT_OUT_SLICES && order != PIFFT_OUT_BITREV)
         return fail("unknown flags %d", flags);
-    if (flags == PIFFT_OUT_NATURAL && count != workers)
+    if (order == PIFFT_OUT_NATURAL && count != workers)
         return fail("natural-order output needs all workers on one plan (use PIFFT_OUT_SLICES)");
     if (!dry) {
         int ndev = 0;
@@ -883,8 +892,9 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
     p->prec = prec;
     p->device = device;
     p->flags = flags;
-    p->natural = (flags == PIFFT_OUT_NATURAL);
-    p->bitrev = (flags == PIFFT_OUT_BITREV);
+    p->natural = (order == PIFFT_OUT_NATURAL);
+    p->bitrev = (order == PIFFT_OUT_BITREV);
+    p->separate_tree = (flags & PIFFT_SEPARATE_TREE) != 0;
     p->esz = prec == PIFFT_F64 ? 16 : 8;
     p->lp = ilog2u(workers);
     p->log_n = ilog2u(n);
@@ -1001,22 +1011,20 @@ void scatter_to_host(const pifft_plan* p, const char* res, char* host_out) {
     const size_t esz = p->esz;
     const uint64_t M = p->m;
     // a plan holding only some workers: its bins go to their stride-P
-    // natural-order positions (other positions untouched, CPU.c:496-499);
-    // typed element copies (one 8/16-B move each, not a memcpy call)
+    // natural-order positions (other positions untouched, CPU.c:496-499).
+    // host_out is a plain C buffer (a double _Complex / float _Complex array is
+    // only 8- / 4-byte aligned): element-sized memcpy, which the compiler
+    // lowers to plain moves without assuming cx<T>'s 16- / 8-byte alignment
     for (uint32_t bt = 0; bt < p->batch; bt++) {
         for (uint32_t q = p->q0; q < p->q0 + p->nq; q++) {
             const uint64_t r = bitrev(q, p->lp);
-            const uint64_t so = (uint64_t)bt * p->nq * M + (uint64_t)(q - p->q0) * M;
-            const uint64_t d0 = (uint64_t)bt * p->n + r;
-            if (esz == 16) {
-                const cx<double>* s = reinterpret_cast<const cx<double>*>(res) + so;
-                cx<double>* d = reinterpret_cast<cx<double>*>(host_out) + d0;
-                for (uint64_t k = 0; k < M; k++) d[k * p->P] = s[k];
-            } else {
-                const cx<float>* s = reinterpret_cast<const cx<float>*>(res) + so;
-                cx<float>* d = reinterpret_cast<cx<float>*>(host_out) + d0;
-                for (uint64_t k = 0; k < M; k++) d[k * p->P] = s[k];
-            }
+            const char* s = res + ((uint64_t)bt * p->nq * M + (uint64_t)(q - p->q0) * M) * esz;
+            char* d = host_out + ((uint64_t)bt * p->n + r) * esz;
+            const uint64_t dstride = (uint64_t)p->P * esz;
+            if (esz == 16)
+                for (uint64_t k = 0; k < M; k++) memcpy(d + k * dstride, s + k * 16, 16);
+            else
+                for (uint64_t k = 0; k < M; k++) memcpy(d + k * dstride, s + k * 8, 8);
         }
     }
 }
@@ -1097,12 +1105,40 @@ int gather_group(pifft_plan* const* plans, int np, const void* const* d_slices, 
     const pifft_plan* p0 = plans[0];
     const uint64_t N = p0->n, M = p0->m;
     const size_t esz = p0->esz;
+    // every destination is written (interleave) while other destinations'
+    // copy streams may still read the sources: no destination may overlap
+    // any source buffer (or another destination)
+    auto overlap = [](const void* a, size_t na, const void* b, size_t nb) {
+        const char *x = (const char*)a, *y = (const char*)b;
+        return x < y + nb && y < x + na;
+    };
+    const size_t nat_bytes = (size_t)p0->batch * N * esz;
+    for (int j = 0; j < np; j++) {
+        if (!d_natural[j]) continue;
+        for (int i = 0; i < np; i++) {
+            const size_t sb = (size_t)out_elems(plans[i]) * esz;
+            if (overlap(d_natural[j], nat_bytes, d_slices[i], sb))
+                return fail("d_natural[%d] overlaps d_slices[%d]: destinations must be distinct from every source", j, i);
+            if (i < j && d_natural[i] && overlap(d_natural[j], nat_bytes, d_natural[i], nat_bytes))
+                return fail("d_natural[%d] overlaps d_natural[%d]", j, i);
+        }
+    }
+    // the copy schedule (pifft_gather.h; its multi-device logic is unit-tested on the CPU)
+    std::vector<GatherSrc> srcs;
+    std::vector<bool> has_dst;
+    for (int i = 0; i < np; i++) {
+        srcs.push_back({plans[i]->device, plans[i]->q0, plans[i]->nq});
+        has_dst.push_back(d_natural[i] != nullptr);
+    }
+    const GatherSchedule gs = gather_schedule(srcs, has_dst, N, M, p0->batch);
     for (int j = 0; j < np; j++) {
         if (!d_natural[j]) continue;
         pifft_plan* d = plans[j];
         DeviceGuard g(d->device);
         if (!d->d_gather) HIPCHK(hipMalloc(&d->d_gather, (size_t)d->batch * N * esz));
-        while ((int)d->gst.size() < np) {
+        for (const auto& pr : gs.peer)
+            if (pr.first == d->device && enable_peer(d, pr.second)) return -1;
+        while ((int)d->gst.size() < gs.streams) {
             hipStream_t st;
             hipEvent_t ev;
             HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -1113,18 +1149,16 @@ int gather_group(pifft_plan* const* plans, int np, const void* const* d_slices, 
         for (auto& e : d->gev)
             if (!e) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipEventRecord(d->gev[0], d->stream));
-        for (int i = 0; i < np; i++) {
-            const pifft_plan* s = plans[i];
-            if (enable_peer(d, s->device)) return -1;
-            hipStream_t cs = d->gst[i];
-            HIPCHK(hipStreamWaitEvent(cs, d->gev[0], 0));
-            const size_t bytes = (size_t)s->nq * M * esz;
-            for (uint32_t bt = 0; bt < d->batch; bt++) {
-                char* dst = (char*)d->d_gather + ((uint64_t)bt * N + (uint64_t)s->q0 * M) * esz;
-                const char* src = (const char*)d_slices[i] + (uint64_t)bt * bytes;
-                HIPCHK(hipMemcpyPeerAsync(dst, d->device, src, s->device, bytes, cs));
-            }
-            HIPCHK(hipEventRecord(d->gdone[i], cs));
+        for (int i = 0; i < gs.streams; i++) HIPCHK(hipStreamWaitEvent(d->gst[i], d->gev[0], 0));
+        for (const GatherCopy& c : gs.copies) {
+            if (c.dst != j) continue;
+            const pifft_plan* s = plans[c.src];
+            HIPCHK(hipMemcpyPeerAsync((char*)d->d_gather + c.dst_off * esz, d->device,
+                                      (const char*)d_slices[c.src] + c.src_off * esz, s->device, c.elems * esz,
+                                      d->gst[c.stream]));
+        }
+        for (int i = 0; i < gs.streams; i++) {
+            HIPCHK(hipEventRecord(d->gdone[i], d->gst[i]));
             HIPCHK(hipStreamWaitEvent(d->stream, d->gdone[i], 0));
         }
         if (launch_interleave(d->d_gather, d_natural[j], N, d->P, d->batch, d->prec, d->stream)) return -1;

@@ -20,6 +20,7 @@ CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64
 OUT_NATURAL, OUT_SLICES, OUT_BITREV = 0, 1, 2
+SEPARATE_TREE = 4  # flag bit: the tree never fused into the first pass (CLI -u)
 KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass", 5: "chunk-a", 6: "chunk-b"}
 MAX_LAUNCH_INFO = 256  # PIFFT_MAX_LAUNCH_INFO (include/pifft.h)
 
@@ -159,6 +160,8 @@ class Plan:
             device = 0 if device is None else device
             if flags is None:
                 flags = OUT_NATURAL if count == workers else OUT_SLICES
+            elif flags == SEPARATE_TREE:
+                flags |= OUT_NATURAL if count == workers else OUT_SLICES
             _check(lib().pifft_plan_create_slices(ctypes.byref(h), n, workers, first, count, batch, prec,
                                                   device, flags), "pifft_plan_create_slices")
         self._h = h

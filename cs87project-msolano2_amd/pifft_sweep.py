@@ -80,9 +80,15 @@ def _ols_noint(X: np.ndarray, y: np.ndarray):
     beta, *_ = np.linalg.lstsq(X, y, rcond=None)
     r = y - X @ beta
     dof = len(y) - X.shape[1]
+    if dof <= 0:  # R: NaN standard errors (no residual degrees of freedom)
+        nan = np.full_like(beta, np.nan)
+        return beta, nan, nan, nan
     s2 = float(r @ r) / dof
     se = np.sqrt(np.diag(s2 * np.linalg.inv(X.T @ X)))
-    tv = beta / se
+    # an exact fit (se == 0): R reports t = +-Inf (p = 0), or NaN for a zero
+    # coefficient -- without numpy's divide-by-zero warning
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tv = beta / se
     pv = 2.0 * stats.t.sf(np.abs(tv), dof)
     return beta, se, tv, pv
 

@@ -56,6 +56,13 @@ extern "C" {
                                one plan this is X in bit-reversed order (no
                                interleave launch) */
 
+#define PIFFT_SEPARATE_TREE 4 /* flag bit, OR-ed with one of the orders above: never
+                               fuse the tree into the first local-FFT pass, so the
+                               stage-1 time is the tree ("funnel") alone, as the
+                               reference's tm_funnel (CPU.c:414-448) -- the column
+                               its cost-law fit regresses on n(p-1)/p
+                               (analyze-results.R:56); CLI -u                  */
+
 typedef struct pifft_plan pifft_plan;
 
 #define PIFFT_MAX_LAUNCH_INFO 256 /* launches described by pifft_plan_info */
@@ -108,7 +115,8 @@ int pifft_plan_create(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t 
 /* Workers [first, first+count) of a P-worker split on `device` (one GPU of a
  * multi-GPU job; the reference's run_thread for each of those Pi).  count must
  * be a power of two dividing first.  flags: PIFFT_OUT_NATURAL (only when
- * count == workers), PIFFT_OUT_SLICES or PIFFT_OUT_BITREV. */
+ * count == workers), PIFFT_OUT_SLICES or PIFFT_OUT_BITREV, optionally with
+ * PIFFT_SEPARATE_TREE. */
 int pifft_plan_create_slices(pifft_plan** plan, uint64_t n, uint32_t workers, uint32_t first,
                              uint32_t count, uint32_t batch, int prec, int device, int flags);
 
@@ -177,7 +185,8 @@ int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int max_launches)
  * CPU.c:414-481).  When a plan evaluates its tree inside the first local-FFT
  * pass (one worker per plan, log2 P <= 4, a multi-pass local FFT; see
  * pifft_plan_info.launch_kind 4) that fused launch cannot be split: stage 1 is
- * then the tree PLUS the first pass, and stage 2 the remaining passes. */
+ * then the tree PLUS the first pass, and stage 2 the remaining passes
+ * (PIFFT_SEPARATE_TREE keeps the tree its own launch). */
 int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double* ms_stage1,
                   double* ms_stage2);
 
@@ -202,7 +211,10 @@ int pifft_execute_group(pifft_plan** plans, int nplans, const void* host_in, voi
  * copied to plan j's device (hipMemcpyPeerAsync over xGMI, one copy stream per
  * source; a device-local copy when both share a device) and interleaved there
  * into natural order: d_natural[j] receives batch*N values.  Call it once the
- * executions that produced d_slices have completed.  Synchronous; ms (may be
+ * executions that produced d_slices have completed.  No d_natural[j] may
+ * overlap any d_slices[i] or another destination (the call fails with -1
+ * otherwise: destinations are written while other copies still read the
+ * sources).  Synchronous; ms (may be
  * NULL) receives the slowest destination's copy + interleave time.  Uses a
  * plan-owned batch*N gather buffer on each destination device. */
 int pifft_allgather(pifft_plan* const* plans, int nplans, const void* const* d_slices, void* const* d_natural,

@@ -454,11 +454,42 @@ def test_fused_tree_first_pass(suf, logn, P, monkeypatch):
         assert "tree" not in kinds, kinds  # fused: no separate tree launch
         got = run(fused, x)
         assert_bins_close(got, pifft_dist.slice_of_natural(want, P, q), suf, n)
-        monkeypatch.setenv("PIFFT_FUSE_TREE", "0")
-        plain = pifft.Plan(n, P, 1, PREC[suf], first=q, count=1, device=0)
-        monkeypatch.delenv("PIFFT_FUSE_TREE")
+        plain = pifft.Plan(n, P, 1, PREC[suf], first=q, count=1, device=0,
+                           flags=pifft.OUT_SLICES | pifft.SEPARATE_TREE)
         assert plain.describe()["launch_kind"][0] == "tree"
         assert rel_l2(run(plain, x), got) <= tol(suf, n)
+
+
+def test_cli_separate_tree_stage_columns(tmp_path):
+    """CLI -u (PIFFT_SEPARATE_TREE): the tree stays its own launch, so the TSV's
+    stage-1 column is the funnel alone (the column analyze-results.R:56 fits
+    on n(p-1)/p); without it a one-worker-per-GPU plan fuses the tree into the
+    first pass (stage 1 = tree + first pass).  Same output either way."""
+    import subprocess
+    cli = pifft.CLI_PATH
+    n, P = 1 << 20, 8
+    outs = {}
+    for flag in ([], ["-u"]):
+        # (one GPU holds all 8 workers here: unfused either way; the stage
+        # split of a one-worker plan is checked through the ABI below)
+        dump = str(tmp_path / f"out{len(flag)}.bin")
+        r = subprocess.run([cli, "-n", str(n), "-p", str(P), "-o", "-f", "64", "-s", "3", "-w", dump] + flag,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        cols = r.stdout.strip().splitlines()[-1].split("\t")
+        assert len(cols) == 5 and float(cols[3]) > 0 and float(cols[4]) > 0
+        outs[bool(flag)] = open(dump, "rb").read()
+    assert outs[True] == outs[False]
+    x = oracle.generate(n, np.complex128, seed=3)
+    fused = pifft.Plan(n, P, 1, pifft.F64, first=0, count=1, device=0)
+    sep = pifft.Plan(n, P, 1, pifft.F64, first=0, count=1, device=0, flags=pifft.OUT_SLICES | pifft.SEPARATE_TREE)
+    assert fused.describe()["launch_kind"][0] == "tree+pass"
+    assert sep.describe()["launch_kind"][:2] == ["tree", "pass"]
+    out = np.zeros(n, np.complex128)
+    t1, t2 = sep.execute(x, out)
+    assert t1 > 0 and t2 > 0
+    assert_bins_close(pifft_dist.slice_of_natural(out, P, 0), pifft_dist.slice_of_natural(oracle.fft(x, P=1), P, 0),
+                      "f64", n)
 
 
 # ------------------------------------------------------------- config 5 ---
@@ -693,6 +724,63 @@ def test_allgather_bitwise_vs_host_scatter(suf, logn, P, per, batch):
         pifft.allgather(plans, [s.data_ptr() for s in slices], dests)
         torch.cuda.synchronize()
         assert torch.equal(nat2, nat)
+
+
+def test_allgather_every_destination_at_once():
+    """Every plan a destination in ONE call (the 8-GPU line's pattern: each
+    destination runs its own copy streams and interleave while the others
+    still read the sources): all destinations bitwise equal to the
+    one-destination result."""
+    n, P = 1 << 16, 8
+    x = oracle.generate(n, np.complex128, seed=7)
+    d_in = dev(x)
+    st = torch.cuda.current_stream()
+    plans = [pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0) for q in range(P)]
+    slices = [torch.empty(p.info.out_elems, dtype=d_in.dtype, device="cuda") for p in plans]
+    for p, sl in zip(plans, slices):
+        p.execute_device(d_in.data_ptr(), sl.data_ptr(), st)
+    torch.cuda.synchronize()
+    one = torch.empty(n, dtype=d_in.dtype, device="cuda")
+    pifft.allgather(plans, [sl.data_ptr() for sl in slices], [one.data_ptr()] + [None] * (P - 1))
+    nats = [torch.empty(n, dtype=d_in.dtype, device="cuda") for _ in range(P)]
+    pifft.allgather(plans, [sl.data_ptr() for sl in slices], [t.data_ptr() for t in nats])
+    torch.cuda.synchronize()
+    for t in nats:
+        assert torch.equal(t, one)
+
+
+def test_allgather_rejects_aliased_destinations():
+    """A destination overlapping a source (or another destination) is refused
+    before any copy is queued."""
+    n, P = 1 << 12, 4
+    plans = [pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0) for q in range(P)]
+    big = torch.zeros(2 * n, dtype=torch.complex128, device="cuda")
+    bufs = [big[q * (n // P):(q + 1) * (n // P)] for q in range(P)]  # the slices: the first n of big
+    nat = torch.empty(n, dtype=torch.complex128, device="cuda")
+    with pytest.raises(pifft.PifftError, match="overlaps d_slices"):
+        pifft.allgather(plans, [b.data_ptr() for b in bufs], [big[n // 2:].data_ptr(), None, None, None])
+    with pytest.raises(pifft.PifftError, match="overlaps d_natural"):
+        pifft.allgather(plans, [b.data_ptr() for b in bufs], [nat.data_ptr(), nat.data_ptr(), None, None])
+    pifft.allgather(plans, [b.data_ptr() for b in bufs], [big[n:].data_ptr(), None, None, None])  # adjacent: fine
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs 2+ GPUs (multi-device placement)")
+@pytest.mark.parametrize("suf", list(DT))
+def test_allgather_plans_on_distinct_devices(suf):
+    """Plan q on GPU q % device_count: the cross-device peer copies (xGMI) and
+    the execute_group input broadcast give the single-device result bit for
+    bit."""
+    ndev = torch.cuda.device_count()
+    n, P, batch = 1 << 16, 8, 2
+    x = oracle.generate(n * batch, DT[suf], seed=5)
+    multi = [pifft.Plan(n, P, batch, PREC[suf], first=q, count=1, device=q % ndev) for q in range(P)]
+    single = [pifft.Plan(n, P, batch, PREC[suf], first=q, count=1, device=0) for q in range(P)]
+    a = np.zeros(n * batch, dtype=DT[suf])
+    b = np.zeros(n * batch, dtype=DT[suf])
+    pifft.execute_group(multi, x, a)
+    pifft.execute_group(single, x, b)
+    assert a.tobytes() == b.tobytes()
 
 
 def test_allgather_errors():

@@ -181,3 +181,16 @@ def test_padded_workspace_rows(monkeypatch):
     small = ws(1 << 28, 8, first=0, count=1, flags=pifft.OUT_SLICES)
     monkeypatch.setenv("PIFFT_W_PAD", "0")
     assert small == ws(1 << 28, 8, first=0, count=1, flags=pifft.OUT_SLICES)
+
+
+def test_separate_tree_flag():
+    """PIFFT_SEPARATE_TREE (CLI -u): a one-worker plan keeps its tree as a
+    separate launch instead of fusing it into the first pass."""
+    n, P = 1 << 24, 8
+    fused = pifft.dry_run(n, P, 1, F64, first=0, count=1)
+    sep = pifft.dry_run(n, P, 1, F64, first=0, count=1, flags=pifft.OUT_SLICES | pifft.SEPARATE_TREE)
+    assert fused["launch_kind"][0] == "tree+pass" and fused["tree_launches"] == 0
+    assert sep["launch_kind"][0] == "tree" and sep["tree_launches"] == 1
+    assert sep["num_passes"] == fused["num_passes"]
+    with pytest.raises(pifft.PifftError, match="unknown flags"):
+        pifft.dry_run(n, P, 1, F64, first=0, count=1, flags=8)

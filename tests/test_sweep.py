@@ -71,3 +71,18 @@ def test_reference_cuda_results_fit():
     res = pifft_sweep.analyze(d)
     assert res["alpha_tr"] < 1e-6 and res["alpha_cy"] < 1e-6
     assert res["speedup"][8192][32] > 10  # 102.8 -> 7.7 ms
+
+
+def test_ols_exact_fit_and_no_dof_without_warnings():
+    """lm(y ~ X - 1) on an exact fit: standard error 0, t = Inf, p = 0 (R's
+    values), with no divide-by-zero warning; and no residual degrees of
+    freedom: NaN standard errors."""
+    import warnings
+    import numpy as np
+    X = np.array([[1.0], [0.0], [0.0]])
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        beta, se, tv, pv = pifft_sweep._ols_noint(X, np.array([3.0, 0.0, 0.0]))
+        assert beta[0] == 3.0 and se[0] == 0.0 and np.isinf(tv[0]) and pv[0] == 0.0
+        beta, se, tv, pv = pifft_sweep._ols_noint(X[:1], np.array([5.0]))
+        assert beta[0] == pytest.approx(5.0) and np.isnan(se[0]) and np.isnan(pv[0])

@@ -2,8 +2,9 @@
 """tools/tune.py -- per-launch GB/s of plan variants in one process.
 
 Each variant is a dict of PIFFT_* planner environment variables (read at plan
-creation).  For each: build the plan, run W warm-ups and K timed executions
-with per-launch HIP events, print per-launch ms and algorithmic GB/s.
+creation).  For each: build the plan, run W warm-ups, replay every launch K
+times back to back (pifft_time_launch) and time K back-to-back executions;
+print per-launch ms and algorithmic GB/s.
 
 usage: python tools/tune.py --log-n 28 --prec 64 --variants '[{"PIFFT_COL_C64":"4"}, {}]'
 """
@@ -64,11 +65,9 @@ def main():
         for _ in range(args.warmup):
             plan.execute_device(x.data_ptr(), y.data_ptr())
         torch.cuda.synchronize()
-        sums = [0.0] * d["num_launches"]
-        for _ in range(args.steps):
-            for i, m in enumerate(plan.execute_device_timed(x.data_ptr(), y.data_ptr())):
-                sums[i] += m
-        avg = [s / args.steps for s in sums]
+        # each launch replayed back to back (in-context durations, pifft_time_launch)
+        avg = [plan.time_launch(i, x.data_ptr(), y.data_ptr(), None, max(args.steps, 5))
+               for i in range(d["num_launches"])]
         tot = sum(avg)
         # back-to-back executions, no per-launch events (what bench.py times)
         e0.record()
