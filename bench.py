@@ -27,12 +27,12 @@ it).  Every rank's own time and dominant-kernel roofline go to config.per_rank.
 
 Adds to the JSON line:
   roofline     : the dominant kernel's algorithmic bytes / its mean duration,
-                 vs 8 TB/s.  The duration: after the timed region, each launch
-                 of the plan replayed K times back to back on the launch stream
-                 with events bound to its first and last dispatch
-                 (pifft_time_launch) -- the in-context duration rocprofv3
-                 reports.  Refused (frac null) if the launches take longer than
-                 the measured step.  traffic = PMC-measured HBM bytes per
+                 vs 8 TB/s.  The duration: a profiling loop after the timed
+                 region times one launch per odd execution, round robin, with
+                 events bound to that dispatch (PIFFT_PROFILE_SAMPLED): the
+                 in-context, back-to-back duration rocprofv3 reports.  Refused
+                 (frac null) if the launches take longer than the measured
+                 step.  traffic = PMC-measured HBM bytes per
                  launch from the committed rocprofv3 summary (profiles/)
   cpu_baseline : the reference CPU path (oracle/_ref, compiled from the
                  reference source) at the SAME N, rank 0 of every job, with the
@@ -355,15 +355,23 @@ class Job:
         barrier()
         return time.perf_counter() - t0
 
-    def time_launches(self, reps: int):
-        """Every launch's in-context duration: the launch replayed `reps` times
-        back to back on the launch stream, with events bound to the first and
-        the last dispatch (pifft_time_launch) -- no marker packet between
-        launches (marker events added ~4 us each; kernels isolated by their own
-        events ran 2-5 % faster than back to back, round-3 trace)."""
-        self.avg = [self.plan.time_launch(i, self.x.data_ptr(), self.y.data_ptr(), self.stream, reps)
-                    for i in range(self.desc["num_launches"])]
-        self.reps = reps
+    def time_launches(self, samples: int):
+        """Every launch's in-context duration (ms): a profiling loop after the
+        timed region in which odd executions time one launch each, round
+        robin, with start/stop events bound to that dispatch
+        (PIFFT_PROFILE_SAMPLED) -- every timed dispatch runs back to back
+        after untimed ones, as in the timed loop (a timed dispatch delays the
+        next by ~9 us; launches timed one after another ran 1-6 % faster than
+        back to back, round-3 trace).  `samples` per launch."""
+        nl = self.desc["num_launches"]
+        execs = 2 * nl * samples
+        self.plan.profile_start(execs, self.pifft.PROFILE_SAMPLED)
+        for _ in range(execs):
+            self.step()
+        used, sums, cnt = self.plan.profile_read()
+        assert used == execs and min(cnt) == samples, (used, cnt)
+        self.avg = [t / c for t, c in zip(sums, cnt)]
+        self.samples = samples
 
     def roofline(self, ms_per_step: float) -> dict:
         """The dominant kernel (the kernel function with the largest share of
@@ -384,8 +392,8 @@ class Job:
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         rec = {"bound": "hbm",
                "kernel": (f"{d['launch_kind'][dom_launches[0]]} kernel of launches {dom_launches} "
-                          f"(mean launch {dom_ms:.4f} ms: each launch replayed back to back on the launch "
-                          f"stream, events bound to the first and last dispatch)"),
+                          f"(mean launch {dom_ms:.4f} ms: events bound to sampled dispatches running back "
+                          f"to back on the launch stream)"),
                "launches": dom_launches, "mean_ms": round(dom_ms, 5),
                "kernel_name": self.plan.kernel_name(dom_launches[0]),
                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -441,7 +449,7 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             k = max(steps, 50) if g["log_n"] < 24 else max(steps, 20)
             elapsed = job.run(k, max(warmup, 5))
             ms = elapsed * 1e3 / k
-            job.time_launches(k)
+            job.time_launches(max(5, k // 2))
             flops = 5.0 * n * g["log_n"] * g["batch"]
             rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
                         "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],
@@ -507,7 +515,7 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
     local_s = job.run(steps, warmup, barrier)
     elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms = elapsed * 1e3 / steps
-    job.time_launches(steps)
+    job.time_launches(max(3, steps))
     rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
                 "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(),
                 "roofline_rank0": job.roofline(local_s * 1e3 / steps) if rank == 0 else None})
@@ -543,7 +551,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
             local_s = job.run(k, max(warmup, 5), barrier)
             elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
             ms = elapsed * 1e3 / k
-            job.time_launches(k)
+            job.time_launches(max(5, k // 2))
             rec.update({"value": round(5.0 * (1 << log_n) * log_n * batch / (ms * 1e-3) / 1e9, 2),
                         "unit": "GFLOP/s", "ms_per_step": round(ms, 6), "steps": k, "n_gpus": world,
                         "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"],
@@ -680,7 +688,7 @@ def main() -> int:
     local_s = job.run(args.steps, args.warmup, barrier)
     elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
     ms_per_step = elapsed * 1e3 / args.steps
-    job.time_launches(args.steps)  # after the timed region: each launch replayed K times
+    job.time_launches(max(5, args.steps // 2))  # after the timed region
     rf = job.roofline(local_s * 1e3 / args.steps)
     desc = job.desc
     launches = job.launches()

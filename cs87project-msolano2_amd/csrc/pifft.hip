@@ -154,8 +154,8 @@ struct pifft_plan {
     int tree_steps = 0, npasses = 0;
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
     std::vector<Step> tree_only;  // the tree stage alone, for pifft_tree_device
-    std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: steps x 2 launches (start, stop of each)
-    int prof_steps = 0, prof_used = 0;
+    std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: per recorded execution, a start and a stop per timed launch
+    int prof_steps = 0, prof_used = 0, prof_mode = 0;
     int radix[8] = {0}, lines[8] = {0}, vpt[8] = {0};
     void* buf[NBUF] = {nullptr};
     size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0, bytes_ch = 0;
@@ -172,7 +172,6 @@ struct pifft_plan {
     std::vector<hipStream_t> gst;  // pifft_allgather: one copy stream per source plan
     std::vector<hipEvent_t> gdone;  // ... and its completion event
     hipEvent_t gev[2] = {nullptr, nullptr};  // gather start / end on `stream`
-    hipEvent_t rep_ev[2] = {nullptr, nullptr};  // pifft_time_launch: first dispatch's start, last one's stop
 };
 
 namespace {
@@ -306,7 +305,8 @@ int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines,
     while (C > 1 && (uint64_t)C > ntrans_lines_cap && R > 8) C /= 2;
     // fill the chip: at least ~2 workgroups per CU (small transforms)
     const uint64_t min_wg = (uint64_t)env_int("PIFFT_MIN_WORKGROUPS", 512);
-    const int cmin = mode == 0 ? 1 : 4;  // strided passes are instantiated for C >= 4
+    // strided passes are instantiated for C >= 4 (and fp64 C = 2 at R = 512-2048, PIFFT_STRIDED_CMIN=2)
+    const int cmin = mode == 0 ? 1 : env_int("PIFFT_STRIDED_CMIN", 4);
     while (C > cmin && R > 8 && total_lines / (uint64_t)C < min_wg) C /= 2;
     while (C > cmin && !find_pass(prec, R, C, mode)) C /= 2;
     return C;
@@ -463,8 +463,6 @@ void release(pifft_plan* p) {
     for (auto st : p->gst) (void)hipStreamDestroy(st);
     for (auto e : p->gdone) (void)hipEventDestroy(e);
     for (auto e : p->gev)
-        if (e) (void)hipEventDestroy(e);
-    for (auto e : p->rep_ev)
         if (e) (void)hipEventDestroy(e);
     for (auto e : p->ev) (void)hipEventDestroy(e);
     for (auto e : p->prof_ev) (void)hipEventDestroy(e);
@@ -1269,39 +1267,33 @@ int pifft_plan_kernel_name(const pifft_plan* p, int launch, char* buf, size_t le
     return 0;
 }
 
+// the launch an execution of a PIFFT_PROFILE_SAMPLED run times (or -1):
+// odd executions time one launch each, round robin, so every timed dispatch
+// follows an untimed one (a timed dispatch delays the next one by ~9 us and
+// would isolate it)
+int sampled_launch(int k, size_t ns) { return (k & 1) ? (int)(((size_t)k >> 1) % ns) : -1; }
+
 int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* stream) {
     if (check_buffers(p, d_in, d_out)) return -1;
     DeviceGuard g(p->device);
     hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
-    hipEvent_t* ev = nullptr;
-    if (p->prof_used < p->prof_steps) ev = &p->prof_ev[(size_t)p->prof_used++ * 2 * p->steps.size()];
-    return launch_steps(p, d_in, d_out, st, ev);
-}
-
-int pifft_time_launch(pifft_plan* p, int launch, const void* d_in, void* d_out, void* stream, int reps,
-                      float* ms_avg) {
-    if (check_buffers(p, d_in, d_out)) return -1;
-    if (launch < 0 || launch >= (int)p->steps.size()) return fail("launch %d out of range", launch);
-    if (reps < 1 || !ms_avg) return fail("bad arguments");
-    DeviceGuard g(p->device);
-    hipStream_t st = (hipStream_t)stream;
-    if (p->rep_ev[0] == nullptr)
-        for (auto& e : p->rep_ev) HIPCHK(hipEventCreate(&e));
-    const Step& s = p->steps[(size_t)launch];
-    for (int r = 0; r < reps; r++)
-        if (launch_step(p, s, d_in, d_out, st, r == 0 ? p->rep_ev[0] : nullptr, r == reps - 1 ? p->rep_ev[1] : nullptr))
-            return -1;
-    HIPCHK(hipEventSynchronize(p->rep_ev[1]));
-    float ms = 0.0f;
-    HIPCHK(hipEventElapsedTime(&ms, p->rep_ev[0], p->rep_ev[1]));
-    *ms_avg = ms / (float)reps;
+    const size_t ns = p->steps.size();
+    if (p->prof_used >= p->prof_steps) return launch_steps(p, d_in, d_out, st, nullptr);
+    const int k = p->prof_used++;
+    if (p->prof_mode == PIFFT_PROFILE_ALL) return launch_steps(p, d_in, d_out, st, &p->prof_ev[(size_t)k * 2 * ns]);
+    const int li = sampled_launch(k, ns);
+    for (size_t i = 0; i < ns; i++) {
+        hipEvent_t* e = (int)i == li ? &p->prof_ev[(size_t)k * 2] : nullptr;
+        if (launch_step(p, p->steps[i], d_in, d_out, st, e ? e[0] : nullptr, e ? e[1] : nullptr)) return -1;
+    }
     return 0;
 }
 
-int pifft_profile_start(pifft_plan* p, int steps) {
+int pifft_profile_start(pifft_plan* p, int steps, int mode) {
     if (!p || steps < 0) return fail("bad arguments");
+    if (mode != PIFFT_PROFILE_ALL && mode != PIFFT_PROFILE_SAMPLED) return fail("unknown profile mode %d", mode);
     DeviceGuard g(p->device);
-    const size_t need = (size_t)steps * 2 * p->steps.size();
+    const size_t need = (size_t)steps * 2 * (mode == PIFFT_PROFILE_ALL ? p->steps.size() : 1);
     while (p->prof_ev.size() < need) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -1309,23 +1301,38 @@ int pifft_profile_start(pifft_plan* p, int steps) {
     }
     p->prof_steps = steps;
     p->prof_used = 0;
+    p->prof_mode = mode;
     return 0;
 }
 
-int pifft_profile_read(pifft_plan* p, float* launch_ms_sum, int max_launches) {
+int pifft_profile_read(pifft_plan* p, float* launch_ms_sum, int* launch_samples, int max_launches) {
     if (!p) return fail("plan is NULL");
     DeviceGuard g(p->device);
     const size_t ns = p->steps.size();
     const int used = p->prof_used;
     p->prof_steps = p->prof_used = 0;  // profiling stops, also on an error below
     std::vector<float> sum(ns, 0.0f), ms;
+    std::vector<int> cnt(ns, 0);
     for (int k = 0; k < used; k++) {
         // each execution's own events: the executions may have run on different streams
-        if (read_launch_ms(ns, &p->prof_ev[(size_t)k * 2 * ns], ms)) return -1;
-        for (size_t i = 0; i < ns; i++) sum[i] += ms[i];
+        if (p->prof_mode == PIFFT_PROFILE_ALL) {
+            if (read_launch_ms(ns, &p->prof_ev[(size_t)k * 2 * ns], ms)) return -1;
+            for (size_t i = 0; i < ns; i++) sum[i] += ms[i], cnt[i]++;
+        } else {
+            const int li = sampled_launch(k, ns);
+            if (li < 0) continue;
+            hipEvent_t* e = &p->prof_ev[(size_t)k * 2];
+            float t = 0.0f;
+            HIPCHK(hipEventSynchronize(e[1]));
+            HIPCHK(hipEventElapsedTime(&t, e[0], e[1]));
+            sum[(size_t)li] += t;
+            cnt[(size_t)li]++;
+        }
     }
-    if (launch_ms_sum)
-        for (int i = 0; i < max_launches && i < (int)ns; i++) launch_ms_sum[i] = sum[i];
+    for (int i = 0; i < max_launches && i < (int)ns; i++) {
+        if (launch_ms_sum) launch_ms_sum[i] = sum[(size_t)i];
+        if (launch_samples) launch_samples[i] = cnt[(size_t)i];
+    }
     return used;
 }
 

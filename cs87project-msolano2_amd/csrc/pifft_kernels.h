@@ -163,29 +163,55 @@ __device__ __forceinline__ void dft(cx<T>* v) {
 // intermediate stays in the Infinity Cache, see PassArgs)
 constexpr bool nt_loads(int nt) { return nt == 1 || nt == 2; }
 constexpr bool nt_stores(int nt) { return nt == 1 || nt == 3; }
-// (the complex value moves as ONE 8- or 16-byte vector: two scalar nt
-// accesses merged by the compiler left fp32 loads waiting on each other)
+// PIFFT_VEC_NT: a complex value moves as ONE 8- or 16-byte vector access
+// (1: both precisions, 2: fp32 only, 0: two scalar nt accesses, which the
+// compiler merges -- for fp32 into loads that waited on each other)
+#ifndef PIFFT_VEC_NT
+#define PIFFT_VEC_NT 1
+#endif
 template <typename T>
 using vec2_t = T __attribute__((ext_vector_type(2)));
+template <typename T>
+constexpr bool vec_nt() {
+    return PIFFT_VEC_NT == 1 || (PIFFT_VEC_NT == 2 && sizeof(T) == 4);
+}
 template <bool NTS, typename T>
 __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
-    if constexpr (NTS && PIFFT_NT_LOADS) {
+    if constexpr (NTS && PIFFT_NT_LOADS && vec_nt<T>()) {
         const vec2_t<T> r = __builtin_nontemporal_load(reinterpret_cast<const vec2_t<T>*>(p));
         return cx<T>{r.x, r.y};
+    } else if constexpr (NTS && PIFFT_NT_LOADS) {
+        cx<T> r;
+        r.re = __builtin_nontemporal_load(&p->re);
+        r.im = __builtin_nontemporal_load(&p->im);
+        return r;
     } else {
         return *p;
     }
 }
 template <bool NTS, typename T>
 __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
-    if constexpr (NTS && PIFFT_NT_STORES) {
+    if constexpr (NTS && PIFFT_NT_STORES && vec_nt<T>()) {
         vec2_t<T> r;
         r.x = v.re;
         r.y = v.im;
         __builtin_nontemporal_store(r, reinterpret_cast<vec2_t<T>*>(p));
+    } else if constexpr (NTS && PIFFT_NT_STORES) {
+        __builtin_nontemporal_store(v.re, &p->re);
+        __builtin_nontemporal_store(v.im, &p->im);
     } else {
         *p = v;
     }
+}
+// PIFFT_CLAMP_LOADS: a partial last tile's idle lanes load the last line again
+// (unconditional loads, no per-load branch; 1: both precisions, 2: fp32 only)
+// instead of skipping their loads
+#ifndef PIFFT_CLAMP_LOADS
+#define PIFFT_CLAMP_LOADS 1
+#endif
+template <typename T>
+constexpr bool clamp_loads() {
+    return PIFFT_CLAMP_LOADS == 1 || (PIFFT_CLAMP_LOADS == 2 && sizeof(T) == 4);
 }
 
 // two-level twiddle: w_M^E = hi[E >> h] * lo[E & (2^h - 1)]
@@ -741,10 +767,11 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int u = 0; u < U; u++) {
             int c, b;
             St::map(tid, u, c, b);
-            // a partial last tile loads the last line again for its idle lanes
-            // (their results are never stored): unconditional loads, no
-            // per-load branch
-            const uint64_t line = tile * C + c < a.nlines ? tile * C + c : a.nlines - 1;
+            // (clamp_loads: idle lanes of a partial last tile load the last
+            // line again -- their results are never stored)
+            constexpr bool CL = clamp_loads<T>();
+            const bool ok = CL || tile * C + c < a.nlines;
+            const uint64_t line = (!CL || tile * C + c < a.nlines) ? tile * C + c : a.nlines - 1;
             const uint64_t bt = line >> log_lb, l = line & lb_mask;
             constexpr bool CHUNK = NTS == 2 || NTS == 3;
             const uint64_t j = (CHUNK && a.rd_virt) ? l : global_line<NTS>(a, l);
@@ -776,7 +803,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                         const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << log_lb);
 #pragma unroll
                         for (int m = 0; m < P; m++)
-                            w[g][m] = ld_stream<nt_loads(NTS)>(leaf + ((uint64_t)m << log_m));
+                            w[g][m] = ok ? ld_stream<nt_loads(NTS)>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
                     }
                     static_for<0, G, 1>([&](auto gc) {
                         constexpr int g = decltype(gc)::value;
@@ -791,11 +818,11 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 const C2* row = in + bin * a.in_bstride + j + (uint64_t)b * rs;
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs);
+                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs) : C2{(T)0, (T)0};
             } else {
 #pragma unroll
                 for (int k = 0; k < q; k++)
-                    v[u * q + k] = ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << les));
+                    v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << les)) : C2{(T)0, (T)0};
             }
         }
     }

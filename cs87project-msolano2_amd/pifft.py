@@ -20,6 +20,7 @@ CLI_PATH = os.path.join(HERE, "pifft")
 
 F32, F64 = 32, 64
 OUT_NATURAL, OUT_SLICES, OUT_BITREV = 0, 1, 2
+PROFILE_ALL, PROFILE_SAMPLED = 0, 1
 SEPARATE_TREE = 4  # flag bit: the tree never fused into the first pass (CLI -u)
 KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass", 5: "chunk-a", 6: "chunk-b"}
 MAX_LAUNCH_INFO = 256  # PIFFT_MAX_LAUNCH_INFO (include/pifft.h)
@@ -83,10 +84,9 @@ _SIGS = {
     "pifft_interleave_device": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                                ctypes.c_int, _P]),
     "pifft_tree_device": (ctypes.c_int, [_P, _P, _P, _P]),
-    "pifft_profile_start": (ctypes.c_int, [_P, ctypes.c_int]),
-    "pifft_time_launch": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, ctypes.c_int,
-                                         ctypes.POINTER(ctypes.c_float)]),
-    "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    "pifft_profile_start": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int]),
+    "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.c_int]),
     "pifft_allgather": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_P),
                                        ctypes.POINTER(ctypes.c_double)]),
 }
@@ -195,24 +195,19 @@ class Plan:
                "pifft_execute_device_timed")
         return list(buf[:n])
 
-    def time_launch(self, launch: int, d_in: int, d_out: int, stream=None, reps: int = 20) -> float:
-        """Mean in-context duration (ms) of one launch replayed `reps` times back to back."""
-        ms = ctypes.c_float()
-        _check(lib().pifft_time_launch(self._h, launch, d_in, d_out, _stream(stream), reps, ctypes.byref(ms)),
-               "pifft_time_launch")
-        return ms.value
+    def profile_start(self, steps: int, mode: int = 1) -> None:
+        """mode PROFILE_SAMPLED (default; in-context) or PROFILE_ALL (isolated)."""
+        _check(lib().pifft_profile_start(self._h, steps, mode), "pifft_profile_start")
 
-    def profile_start(self, steps: int) -> None:
-        _check(lib().pifft_profile_start(self._h, steps), "pifft_profile_start")
-
-    def profile_read(self) -> tuple[int, list[float]]:
-        """(executions recorded, per-launch ms summed over them)."""
+    def profile_read(self) -> tuple[int, list[float], list[int]]:
+        """(executions recorded, per-launch ms summed over its samples, samples per launch)."""
         n = self.info.num_launches
         buf = (ctypes.c_float * max(n, 1))()
-        used = lib().pifft_profile_read(self._h, buf, n)
+        cnt = (ctypes.c_int * max(n, 1))()
+        used = lib().pifft_profile_read(self._h, buf, cnt, n)
         if used < 0:
             raise PifftError(f"pifft_profile_read: {last_error()}")
-        return used, list(buf[:n])
+        return used, list(buf[:n]), list(cnt[:n])
 
     def execute(self, host_in, host_out=None):
         """numpy in -> natural-order numpy out (only this plan's bins written)."""

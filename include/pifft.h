@@ -152,27 +152,27 @@ int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* 
 int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, void* stream,
                                float* launch_ms, int max_launches);
 
-/* In-context duration of one launch (< info.num_launches): the launch alone,
- * `reps` times back to back on `stream` (the buffers and workspace as an
- * execution of the plan leaves them), with a start event bound to the first
- * dispatch and a stop event to the last (hipExtLaunchKernel), so no marker
- * packet or event isolates the launches; *ms_avg = elapsed / reps.  Kernels
- * timed one at a time with their own events (pifft_profile_*) run 2-5 %
- * faster than back to back in a stream, where rocprofv3 and the step time see
- * them (round-3 trace).  Synchronous. */
-int pifft_time_launch(pifft_plan* plan, int launch, const void* d_in, void* d_out, void* stream, int reps,
-                      float* ms_avg);
-
-/* Asynchronous per-launch timing: after pifft_profile_start(plan, steps),
- * each of the next `steps` pifft_execute_device calls binds a start and a stop
- * event to every launch (kernel-bound, as pifft_execute_device_timed; no host
- * sync, nothing added to the stream);
- * pifft_profile_read waits for every recorded execution's last event, writes
- * the per-launch duration summed over the recorded executions to
- * launch_ms_sum[0 .. min(num_launches, max_launches)), stops profiling (also
- * when it fails) and returns the number of executions recorded (or -1). */
-int pifft_profile_start(pifft_plan* plan, int steps);
-int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int max_launches);
+/* Asynchronous per-launch timing.  After pifft_profile_start(plan, steps,
+ * mode) the next `steps` pifft_execute_device calls bind start/stop events to
+ * launches (hipExtLaunchKernel: the dispatch's own timestamps, as rocprofv3
+ * reports them; no host sync):
+ *   PIFFT_PROFILE_ALL     every launch of every execution.  A timed dispatch
+ *                         delays the next one by ~9 us, so the launches run
+ *                         isolated -- 1-6 % faster than back to back;
+ *   PIFFT_PROFILE_SAMPLED in-context: execution k times launch (k/2) mod L
+ *                         when k is odd and nothing when k is even, so every
+ *                         timed dispatch follows untimed ones, back to back
+ *                         as in an unprofiled run (what bench.py's roofline
+ *                         uses; steps = 2 L s gives s samples per launch).
+ * pifft_profile_read waits for the recorded executions, writes each launch's
+ * summed duration (ms) and sample count to launch_ms_sum / launch_samples
+ * (either may be NULL; the first min(num_launches, max_launches) launches),
+ * stops profiling (also when it fails) and returns the number of executions
+ * recorded (or -1).  The profiled executions' own step time is NOT clean. */
+#define PIFFT_PROFILE_ALL 0
+#define PIFFT_PROFILE_SAMPLED 1
+int pifft_profile_start(pifft_plan* plan, int steps, int mode);
+int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int* launch_samples, int max_launches);
 
 /* Host boundary, the reference's run() shape: copies host_in (batch*N values)
  * to the device (untimed), runs, and if host_out != NULL writes this plan's

@@ -8,8 +8,10 @@ secondary configs).  Dispatches are split into one cluster per config at each
 input generation (k_generate: every config's Job starts with one; its warm-up,
 timed and clean loops follow).  For each roofline the dominant kernel (by the
 demangled name bench.py records, pifft_plan_kernel_name) is averaged over its
-cluster's dispatches and over all dispatches of that name (what --stats
-prints), and the bench line's mean launch time is compared with both.
+cluster's back-to-back dispatches (those starting within BACK_TO_BACK_US of the
+previous dispatch's end: the timed loop's context) and over all dispatches of
+that name (what --stats prints); the bench line's mean launch time is compared
+with the first.
 Done when every frac is within 3 % of rocprof's."""
 import csv
 import glob
@@ -19,6 +21,7 @@ import sqlite3
 import sys
 
 TOL = 0.03
+BACK_TO_BACK_US = 2.0
 
 
 def rooflines(line):
@@ -40,12 +43,14 @@ def main():
             avg = r.get("AverageNs") or r.get("Average (Nsec)")
             stats[r["Name"]] = (int(r["Calls"]), float(avg) * 1e-6)
     con = sqlite3.connect(sys.argv[3])
-    clusters = []
+    clusters, last_end = [], None
     for n, s, e in con.execute("select name, start, end from kernels order by start"):
+        gap = (s - last_end) * 1e-3 if last_end is not None else 1e9  # us since the previous dispatch ended
+        last_end = e
         if "k_generate" in n:  # every config (bench.py Job) starts by generating its input
             clusters.append([])
         elif clusters:
-            clusters[-1].append((n, (e - s) * 1e-6))
+            clusters[-1].append((n, (e - s) * 1e-6, gap))
     rfs = rooflines(line)
     print(f"{len(clusters)} dispatch clusters in the trace, {len(rfs)} rooflines in the line")
     worst, ok = 0.0, True
@@ -58,7 +63,9 @@ def main():
             ok = False
             continue
         cl = clusters[i] if i < len(clusters) else []
-        durs = [d for n, d in cl if n == name]
+        # back-to-back dispatches only (the timed loop's context; a dispatch
+        # after one with bound events starts ~9 us late, isolated)
+        durs = [d for n, d, gap in cl if n == name and gap < BACK_TO_BACK_US]
         tr = sum(durs) / len(durs) if durs else None
         st = stats.get(name, (0, None))[1]
         ref = tr if tr is not None else st

@@ -61,10 +61,10 @@ def main():
                 for _ in range(2):
                     plan.execute_device(x, y, s)
                 torch.cuda.synchronize()
-                plan.profile_start(STEPS)
+                plan.profile_start(STEPS, pifft.PROFILE_ALL)
                 for _ in range(STEPS):
                     plan.execute_device(x, y, s)
-                used, sums = plan.profile_read()
+                used, sums, _ = plan.profile_read()
                 ms = [v / used for v in sums]
                 print(f"flags {flags} trial {t} rep {rep} x={x & ((1 << 32) - 1):#010x} y={y & ((1 << 32) - 1):#010x}"
                       f"  passes " + " ".join(f"{v:.3f}" for v in ms) + f"  total {sum(ms):.3f} ms", flush=True)
@@ -88,10 +88,10 @@ def which_buffer():
         for _ in range(2):
             plan.execute_device(x, yy, s)
         torch.cuda.synchronize()
-        plan.profile_start(STEPS)
+        plan.profile_start(STEPS, pifft.PROFILE_ALL)
         for _ in range(STEPS):
             plan.execute_device(x, yy, s)
-        used, sums = plan.profile_read()
+        used, sums, _ = plan.profile_read()
         ms = [v / used for v in sums]
         print(f"{tag} passes " + " ".join(f"{v:.3f}" for v in ms) + f"  total {sum(ms):.3f} ms", flush=True)
 

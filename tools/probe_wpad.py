@@ -53,10 +53,10 @@ def main():
                 for _ in range(2):
                     plan.execute_device(x.data_ptr(), y.data_ptr(), s)
                 torch.cuda.synchronize()
-                plan.profile_start(STEPS)
+                plan.profile_start(STEPS, pifft.PROFILE_ALL)
                 for _ in range(STEPS):
                     plan.execute_device(x.data_ptr(), y.data_ptr(), s)
-                used, sums = plan.profile_read()
+                used, sums, _ = plan.profile_read()
                 ms = [v / used for v in sums]
                 if best is None or sum(ms) < sum(best):
                     best = ms

@@ -2,9 +2,9 @@
 """tools/tune.py -- per-launch GB/s of plan variants in one process.
 
 Each variant is a dict of PIFFT_* planner environment variables (read at plan
-creation).  For each: build the plan, run W warm-ups, replay every launch K
-times back to back (pifft_time_launch) and time K back-to-back executions;
-print per-launch ms and algorithmic GB/s.
+creation).  For each: build the plan, run W warm-ups, time every launch in
+context (PIFFT_PROFILE_SAMPLED) and K back-to-back executions; print
+per-launch ms and algorithmic GB/s.
 
 usage: python tools/tune.py --log-n 28 --prec 64 --variants '[{"PIFFT_COL_C64":"4"}, {}]'
 """
@@ -65,9 +65,14 @@ def main():
         for _ in range(args.warmup):
             plan.execute_device(x.data_ptr(), y.data_ptr())
         torch.cuda.synchronize()
-        # each launch replayed back to back (in-context durations, pifft_time_launch)
-        avg = [plan.time_launch(i, x.data_ptr(), y.data_ptr(), None, max(args.steps, 5))
-               for i in range(d["num_launches"])]
+        # in-context per-launch durations: sampled dispatches back to back (PIFFT_PROFILE_SAMPLED)
+        samples = max(args.steps // 2, 3)
+        execs = 2 * d["num_launches"] * samples
+        plan.profile_start(execs, pifft.PROFILE_SAMPLED)
+        for _ in range(execs):
+            plan.execute_device(x.data_ptr(), y.data_ptr())
+        _, sums, cnt = plan.profile_read()
+        avg = [t / c for t, c in zip(sums, cnt)]
         tot = sum(avg)
         # back-to-back executions, no per-launch events (what bench.py times)
         e0.record()
