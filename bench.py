@@ -30,9 +30,10 @@ Adds to the JSON line:
                  vs 8 TB/s.  The duration: a profiling loop after the timed
                  region times one launch per odd execution, round robin, with
                  events bound to that dispatch (PIFFT_PROFILE_SAMPLED): the
-                 in-context, back-to-back duration rocprofv3 reports.  Refused
-                 (frac null) if the launches take longer than the measured
-                 step.  traffic = PMC-measured HBM bytes per
+                 in-context, back-to-back duration rocprofv3 reports; event
+                 overhead beyond the measured step is subtracted in proportion
+                 (Job.scaled).  Refused (frac null) if the launches still take
+                 longer than the step.  traffic = PMC-measured HBM bytes per
                  launch from the committed rocprofv3 summary (profiles/)
   cpu_baseline : the reference CPU path (oracle/_ref, compiled from the
                  reference source) at the SAME N, rank 0 of every job, with the
@@ -379,8 +380,10 @@ class Job:
         algorithmic bytes per launch / its mean launch duration.  Self-check:
         no frac is emitted when that kernel's time per step (or all launches'
         time) exceeds the measured step time."""
-        d, avg = self.desc, self.avg
+        d = self.desc
         nl = d["num_launches"]
+        raw_step_ms = sum(self.avg[:nl])
+        avg = self.scaled(ms_per_step)
         by_fn = {}
         for i in range(nl):
             by_fn.setdefault(d["launch_fn"][i], []).append(i)
@@ -399,19 +402,33 @@ class Job:
                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": dom_bytes,
                "kernel_ms_per_step": round(dom_step_ms, 6), "all_launches_ms_per_step": round(kernel_step_ms, 6),
-               "step_ms": round(ms_per_step, 6)}
-        if dom_ms <= 0 or dom_step_ms > ms_per_step or kernel_step_ms > ms_per_step:
+               "step_ms": round(ms_per_step, 6), "event_ms_per_step": round(raw_step_ms, 6),
+               "event_overhead_subtracted_ms": round(raw_step_ms - kernel_step_ms, 6)}
+        if dom_ms <= 0 or dom_step_ms > ms_per_step * (1 + 1e-9) or kernel_step_ms > ms_per_step * (1 + 1e-9):
             rec.update({"achieved": None, "frac": None,
                         "error": f"refused: launches take {kernel_step_ms:.6f} ms (dominant {dom_step_ms:.6f} ms) "
                                  f"per {ms_per_step:.6f}-ms step"})
         return rec
 
-    def launches(self) -> list:
+    def scaled(self, ms_per_step: float) -> list:
+        """Per-launch ms with the event overhead taken out: a dispatch with
+        bound events runs a little longer than an unbound one (its timestamps
+        wait for the end-of-kernel release), so when the launches' event
+        times add up to more than the measured step, the excess is subtracted
+        in proportion -- the launches then account for exactly the step."""
+        nl = self.desc["num_launches"]
+        raw = sum(self.avg[:nl])
+        scale = min(1.0, ms_per_step / raw) if raw > 0 else 1.0
+        return [t * scale for t in self.avg]
+
+    def launches(self, ms_per_step: float) -> list:
         d, out = self.desc, []
+        avg = self.scaled(ms_per_step)
         for i in range(d["num_launches"]):
             b = d["launch_bytes"][i]
-            out.append({"kind": d["launch_kind"][i], "bytes": b, "ms": round(self.avg[i], 4),
-                        "GB/s": round(b / (self.avg[i] * 1e-3) / 1e9, 1) if self.avg[i] > 0 else None})
+            out.append({"kind": d["launch_kind"][i], "bytes": b, "ms": round(avg[i], 4),
+                        "event_ms": round(self.avg[i], 4),
+                        "GB/s": round(b / (avg[i] * 1e-3) / 1e9, 1) if avg[i] > 0 else None})
         return out
 
     def free(self):
@@ -454,7 +471,7 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
                         "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],
                         "workers_in_plan": g["count"], "batch": g["batch"], "passes": job.desc["num_passes"],
-                        "radix": job.desc["radix"], "launches": job.launches(), "roofline": job.roofline(ms)})
+                        "radix": job.desc["radix"], "launches": job.launches(ms), "roofline": job.roofline(ms)})
             job.free()
         except Exception as e:  # reported, never silently replaced
             rec["error"] = repr(e)
@@ -517,7 +534,7 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
     ms = elapsed * 1e3 / steps
     job.time_launches(max(3, steps))
     rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
-                "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(),
+                "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(local_s * 1e3 / steps),
                 "roofline_rank0": job.roofline(local_s * 1e3 / steps) if rank == 0 else None})
     job.x = None  # the 64 GiB replica is not needed by the exchange
     job.plan.close()  # nor the plan's workspace
@@ -691,7 +708,7 @@ def main() -> int:
     job.time_launches(max(5, args.steps // 2))  # after the timed region
     rf = job.roofline(local_s * 1e3 / args.steps)
     desc = job.desc
-    launches = job.launches()
+    launches = job.launches(local_s * 1e3 / args.steps)
     config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
     traffic, traffic_src = load_traffic(config_key, rf["launches"])
 

@@ -165,9 +165,12 @@ constexpr bool nt_loads(int nt) { return nt == 1 || nt == 2; }
 constexpr bool nt_stores(int nt) { return nt == 1 || nt == 3; }
 // PIFFT_VEC_NT: a complex value moves as ONE 8- or 16-byte vector access
 // (1: both precisions, 2: fp32 only, 0: two scalar nt accesses, which the
-// compiler merges -- for fp32 into loads that waited on each other)
+// compiler merges -- for fp32 into loads that waited on each other).
+// Measured on MI355X (profiles/r03_ab_kernel_forms.log): fp32 2^28 3.23 ->
+// 3.04 ms with 2 (the same with 1); fp64 2^28 within the box's +-2 % spread
+// either way, so fp64 keeps its round-2 code (2).
 #ifndef PIFFT_VEC_NT
-#define PIFFT_VEC_NT 1
+#define PIFFT_VEC_NT 2
 #endif
 template <typename T>
 using vec2_t = T __attribute__((ext_vector_type(2)));
@@ -205,9 +208,9 @@ __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
 }
 // PIFFT_CLAMP_LOADS: a partial last tile's idle lanes load the last line again
 // (unconditional loads, no per-load branch; 1: both precisions, 2: fp32 only)
-// instead of skipping their loads
+// instead of skipping their loads (same measurements: fp32 only, 2)
 #ifndef PIFFT_CLAMP_LOADS
-#define PIFFT_CLAMP_LOADS 1
+#define PIFFT_CLAMP_LOADS 2
 #endif
 template <typename T>
 constexpr bool clamp_loads() {
@@ -727,6 +730,12 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
     constexpr LdsLayout LL = LdsPick<T, R, C, BM, VPT>::value;
+    // Several butterflies per thread (VPT 32): one after the other, each with
+    // its own twiddles, loads and stores -- scheduling barriers keep the
+    // compiler from interleaving their temporaries and hoisting their
+    // addresses (two concurrent radix-16 DFTs spill at the 128-VGPR budget of
+    // two workgroups per CU)
+    constexpr bool serial = U > 1 && Sh::Q > 16 && PIFFT_SERIAL_BFLY;
     // (run-time even where the mode fixes them -- M/R = 1 for a single pass,
     // Ns = 1 for a first pass: compile-time values measured 2 % slower there)
     const uint32_t log_lb = a.log_lb;
@@ -839,11 +848,6 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             }
         });
     }
-    // Several radix-16 butterflies per thread (VPT 32): one after the other,
-    // each with its own twiddles -- a scheduling barrier keeps the compiler
-    // from interleaving their temporaries (two concurrent radix-16 DFTs spill
-    // at the 128-VGPR budget of two workgroups per CU)
-    constexpr bool serial = U > 1 && Sh::Q > 16 && PIFFT_SERIAL_BFLY;
     // ---- twiddles before the butterflies ----
     if constexpr (St::first && BM == 2) {
         // w_{Ns R}^{(j mod Ns) r}, r = b + k NB: the k-dependent factor
@@ -927,6 +931,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     const uint32_t ks = lns + il;
 #pragma unroll
                     for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << ks), v[u * q + k]);
+                    if constexpr (serial && PIFFT_SERIAL_BFLY >= 2) __builtin_amdgcn_sched_barrier(0);
                 } else {
                     C2* dst = out + bt * a.out_bstride;
                     const uint32_t sh = 64 - (log_lb + Sh::LOGR);  // log2 M bits
