@@ -110,9 +110,10 @@ const std::vector<PassKernel>& pass_kernels() {
     return all;
 }
 
-const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0, int vpt = 16) {
+const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0, int vpt = 16, int h = 1) {
     for (const auto& k : pass_kernels())
-        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt)
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt &&
+            k.h == h)
             return &k;
     return nullptr;
 }
@@ -271,6 +272,7 @@ uint64_t interleave_threads(uint64_t total, int lp, int prec, uint64_t n) {
 struct PassChoice {
     int R, C, mode, nts;
     int vpt = 16;
+    int h = 1;  // sub-tiles per workgroup (k_pass H)
 };
 
 // Tile = R x C elements per workgroup (C adjacent lines of an R-point sub-FFT).
@@ -439,6 +441,17 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         }
     }
     if (out.empty()) return fail("no pass decomposition for M=2^%d", logm);
+    // tuning: two sub-tiles per workgroup on the strided passes (k_pass H = 2,
+    // one workgroup per CU): PIFFT_SUBTILES=2 (every strided pass) or
+    // PIFFT_SUBTILES_FIRST=2 (the first pass only)
+    {
+        const int hall = env_int("PIFFT_SUBTILES", 1), hfirst = env_int("PIFFT_SUBTILES_FIRST", hall);
+        for (size_t i = 0; i < out.size(); i++) {
+            PassChoice& pc = out[i];
+            const int h = (pc.mode == 1) ? hfirst : (pc.mode == 2 ? hall : 1);
+            if (h > 1 && find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, pc.vpt, h)) pc.h = h;
+        }
+    }
     // tuning: fp32 strided passes at 32 values per thread (512 threads over
     // the 16384-value tile, PIFFT_TILE32=16384, two workgroups per CU)
     if (prec == 32 && env_int("PIFFT_VPT32", 0))
@@ -587,6 +600,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
             return fail("no bit-reversed pass kernel R=%d C=%d mode=%d", l.R, l.C, bm);
         l.C = C;
         l.mode = bm | 4;
+        l.h = 1;
     }
 
     // All P workers on this plan, natural order, and an output small enough to
@@ -615,7 +629,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
         p->ilv = on;
     }
-    if (p->ilv) passes.back().nts = 0;
+    if (p->ilv) {
+        passes.back().nts = 0;
+        passes.back().h = 1;
+    }
     TableBuilder tb(esz);
     // --- tree tables (w_N) ---
     const bool need_tree = p->P > 1;
@@ -727,7 +744,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
         const int last_nt = last_pass && passes[i].mode == 2 ? env_int("PIFFT_LAST_NT", -1) : -1;
         const PassKernel* k = fuse_here ? fused
                                         : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode,
-                                                    last_nt >= 0 ? last_nt : passes[i].nts, 0, passes[i].vpt);
+                                                    last_nt >= 0 ? last_nt : passes[i].nts, 0, passes[i].vpt,
+                                                    passes[i].h);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
@@ -764,7 +782,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
             s.pa.log_xg = std::max<uint32_t>(s.pa.log_xg, (uint32_t)env_int("PIFFT_ILV_XCD_GROUP", p->lp));
         }
         s.block = dim3((unsigned)k->nt);
-        const uint64_t wgs = (s.pa.nlines + k->C - 1) / k->C;
+        const uint64_t lines_per_wg = (uint64_t)k->C * k->h;  // H sub-tiles of C lines
+        if (k->h > 1 && (s.pa.nlines % lines_per_wg || s.pa.ilv_log))
+            return fail("sub-tiled pass needs whole workgroups and no natural-order store");
+        const uint64_t wgs = (s.pa.nlines + lines_per_wg - 1) / lines_per_wg;
         if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
                                                              (unsigned long long)(wgs * k->nt));
         s.grid = dim3((unsigned)wgs);
@@ -774,7 +795,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
             (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {
             p->radix[i] = k->R;
-            p->lines[i] = k->C;
+            p->lines[i] = k->C * k->h;
             p->vpt[i] = k->vpt;
         }
         ns *= (uint64_t)k->R;

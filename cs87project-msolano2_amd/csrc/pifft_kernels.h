@@ -716,8 +716,13 @@ constexpr int pre_count() {
 #ifndef PIFFT_SERIAL_BFLY
 #define PIFFT_SERIAL_BFLY 1
 #endif
-template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT>
-__device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, cx<T>* pre, int tid, uint64_t tile) {
+// PH (phase): 0 the whole pass for one tile; 1 only the first stage's loads
+// (and MODE 2's inter-pass twiddle fetch, into twp); 2 everything after them
+// (k_pass with H sub-tiles: every sub-tile's loads first, then one sub-tile
+// after the other)
+template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT, int PH = 0>
+__device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, cx<T>* pre, int tid, uint64_t tile,
+                                            cx<T>* twp) {
     using C2 = cx<T>;
     // MODE | 4: the same pass storing at bitrev_{log2 M}(natural position),
     // the reference's scratch order (PIFFT_OUT_BITREV; last pass only).  Each
@@ -750,8 +755,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     // multiple of C: c does not depend on u) the step factor w^{jm NB} is
     // shared: fetched once, for u = 0.
     constexpr bool share_anc = St::cfast && U > 1 && St::NT % C == 0;
-    [[maybe_unused]] C2 tw_pre[St::first && BM == 2 ? 4 * U : 1];
-    if constexpr (St::first && BM == 2) {
+    [[maybe_unused]] C2* tw_pre = twp;  // 4 U entries (k_pass: first_tw_count)
+    if constexpr (St::first && BM == 2 && PH != 2) {
         const C2* tlo = static_cast<const C2*>(a.tw_lo);
         const C2* thi = static_cast<const C2*>(a.tw_hi);
         const uint64_t hmask = (1ull << a.tw_h) - 1;
@@ -769,7 +774,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             tw_pre[4 * u + 3] = thi[e1 >> a.tw_h];
         }
     }
-    if constexpr (St::first) {
+    if constexpr (St::first && PH != 2) {
         // ---- inputs straight from HBM (all loads issued before any use) ----
         const C2* __restrict__ in = static_cast<const C2*>(a.in);
 #pragma unroll
@@ -835,6 +840,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             }
         }
     }
+    if constexpr (PH == 1) return;
     if constexpr (St::first && tw_prefetch<R, C, BM, VPT>()) {
         const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
         static_for<1, Sh::NSTG, 1>([&](auto sc) {
@@ -960,7 +966,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #pragma unroll
             for (int g = 0; g < 8; g++) pl_swap<16>(v[2 * g], v[2 * g + 1]);
         }
-        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile, twp);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
         using Nx = Stage<R, C, BM, S + 1, VPT>;
@@ -988,8 +994,24 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 }
             }
         }
-        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile);
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile, twp);
     }
+}
+
+// inter-pass twiddle entries fetched with a tile's first-stage loads (MODE 2)
+template <int R, int C, int MODE, int VPT>
+constexpr int first_tw_count() {
+    return (MODE & 3) == 2 ? 4 * Stage<R, C, 2, 0, VPT>::U : 1;
+}
+
+// Workgroups per CU a k_pass instance is built for: two (PIFFT_MIN_WG_PER_CU),
+// one with H = 2 sub-tiles (the second sub-tile's data waits in registers:
+// two fp32 sub-tiles spill at 128 VGPRs)
+template <typename T, int R, int C, int MODE, int LP, int VPT, int H>
+constexpr int pass_waves_per_eu() {
+    constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
+    if constexpr (H > 1) return w > 2 ? w / 2 : w;
+    else return (MODE == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)
@@ -999,28 +1021,53 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
 // NTS: non-temporal streaming of the data (nt_loads / nt_stores)
-template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16>
-__global__ __launch_bounds__((PassCfg<R, C, VPT>::NT),
-                             (MODE == 3 && LP >= 4 && PassCfg<R, C, VPT>::waves_per_eu > 2
-                                  ? 2
-                                  : PassCfg<R, C, VPT>::waves_per_eu))
+// H: sub-tiles per workgroup.  H = 2: the workgroup owns 2 C adjacent lines
+// and issues both halves' loads first (2 C-line row segments on a strided
+// read side, e.g. 256 B for fp64 C = 8), then runs one half's stages and
+// stores while the other half's data waits in registers, then the other half
+// (its stages overlap the first half's stores).  Same LDS as H = 1.
+template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16, int H = 1>
+__global__ __launch_bounds__((PassCfg<R, C, VPT>::NT), (pass_waves_per_eu<T, R, C, MODE, LP, VPT, H>()))
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
-    cx<T> v[PassShape<R, VPT>::Q];
+    constexpr int Q = PassShape<R, VPT>::Q;
+    constexpr int TWN = first_tw_count<R, C, MODE, VPT>();
     cx<T> pre[pre_count<R, C, MODE & 3, VPT>() > 0 ? pre_count<R, C, MODE & 3, VPT>() : 1];
     // one tile per workgroup: a persistent tile loop (1, 2 or 4 resident
     // workgroups per CU walking the tiles) measured 1.4-1.7x slower at 2^28
     // fp64
     uint64_t tile = tile_of_block(blockIdx.x, a.log_xg, gridDim.x);
-    if (a.ilv_log && a.log_lb >= (uint32_t)ilog2c(C)) {
-        // natural-order store: the P workers' tiles of one line block run
-        // back to back (and on one XCD, log_xg >= log2 P), so the P 16-B
-        // pieces of each output line meet in one L2 before it is written
-        const uint32_t il = a.ilv_log, ltt = a.log_lb - (uint32_t)ilog2c(C);  // 2^ltt tiles per transform
-        const uint64_t q = tile & ((1ull << il) - 1), rest = tile >> il;
-        tile = ((rest >> ltt) << (il + ltt)) + (q << ltt) + (rest & ((1ull << ltt) - 1));
+    T* lds = reinterpret_cast<T*>(pifft_smem);
+    const int tid = (int)threadIdx.x;
+    if constexpr (H == 1) {
+        if (a.ilv_log && a.log_lb >= (uint32_t)ilog2c(C)) {
+            // natural-order store: the P workers' tiles of one line block run
+            // back to back (and on one XCD, log_xg >= log2 P), so the P 16-B
+            // pieces of each output line meet in one L2 before it is written
+            const uint32_t il = a.ilv_log, ltt = a.log_lb - (uint32_t)ilog2c(C);  // 2^ltt tiles per transform
+            const uint64_t q = tile & ((1ull << il) - 1), rest = tile >> il;
+            tile = ((rest >> ltt) << (il + ltt)) + (q << ltt) + (rest & ((1ull << ltt) - 1));
+        }
+        cx<T> v[Q];
+        cx<T> twp[TWN];
+        pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, lds, v, pre, tid, tile, twp);
+    } else {
+        cx<T> v[H][Q];
+        cx<T> twp[H][TWN];
+#pragma unroll
+        for (int h = 0; h < H; h++)
+            pass_stages<T, R, C, MODE, NTS, LP, 0, VPT, 1>(a, lds, v[h], pre, tid, tile * H + h, twp[h]);
+        // (scheduling barriers: the sub-tiles run one after the other -- the
+        // compiler would otherwise interleave their independent arithmetic and
+        // hold both sub-tiles' temporaries at once)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < H; h++) {
+            if (h) __syncthreads();  // the previous sub-tile's last LDS reads are done
+            pass_stages<T, R, C, MODE, NTS, LP, 0, VPT, 2>(a, lds, v[h], pre, tid, tile * H + h, twp[h]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
-    pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, reinterpret_cast<T*>(pifft_smem), v, pre, (int)threadIdx.x, tile);
 }
 
 // ---------------------------------------------------------------------------

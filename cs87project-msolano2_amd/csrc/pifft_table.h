@@ -10,6 +10,7 @@ struct PassKernel {
     int nt;
     int lds_bytes;
     int vpt;  // values per thread (16, or 8 for small single-pass launches)
+    int h;    // sub-tiles per workgroup (k_pass H)
 };
 
 }  // namespace pifft

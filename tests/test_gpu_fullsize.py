@@ -222,3 +222,29 @@ def test_reference_max_size_n2e30_fp64():
     torch.cuda.synchronize()
     err2 = (torch.linalg.vector_norm(Z.conj() / n - x) / xn).item()
     assert err2 <= TOL64, err2
+
+
+@pytest.mark.parametrize("prec,passes", [(pifft.F64, "0"), (pifft.F32, "3")])
+def test_subtiled_passes_bitwise_equal(prec, passes, monkeypatch):
+    """k_pass with two sub-tiles per workgroup (H = 2, PIFFT_SUBTILES) runs the
+    same per-line arithmetic as H = 1: the 2^28 plan's output is bitwise
+    equal (fp64 1024-512-512, fp32 forced to the same three passes)."""
+    n = 1 << 28
+    cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=cdt, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, prec, seed=21, stream=st)
+    if passes != "0":
+        monkeypatch.setenv("PIFFT_PASSES", passes)
+    base = pifft.Plan(n, 1, 1, prec)
+    monkeypatch.setenv("PIFFT_SUBTILES", "2")
+    sub = pifft.Plan(n, 1, 1, prec)
+    assert base.describe()["radix"] == sub.describe()["radix"] == [1024, 512, 512]
+    assert [2 * c for c in base.describe()["lines"]] == sub.describe()["lines"]
+    ya = torch.empty_like(x)
+    base.execute_device(x.data_ptr(), ya.data_ptr(), st)
+    base.close()
+    yb = torch.empty_like(x)
+    sub.execute_device(x.data_ptr(), yb.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb))

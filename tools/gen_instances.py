@@ -58,6 +58,13 @@ for T, prec in (("double", 64), ("float", 32)):
             for nts in (0, 1):
                 for lp in (1, 2, 3, 4):
                     items.append(f"PK({T}, {prec}, {R}, {C}, 3, {nts}, {lp}),")
+# two sub-tiles per workgroup (k_pass H = 2, one workgroup per CU): the
+# 2^28 three-pass plans' strided passes with twice the lines per workgroup on
+# the read side (PIFFT_SUBTILES)
+for T, prec in (("double", 64), ("float", 32)):
+    for R, C in ((1024, 8), (512, 16)):
+        for mode in (1, 2):
+            items.append(f"PKVH({T}, {prec}, {R}, {C}, {mode}, 1, 0, 16, 2),")
 # fp64 strided passes at C = 2 for the latency-bound 2^20 sizes (two
 # workgroups of 128 threads per CU instead of one of 256: PIFFT_STRIDED_CMIN=2)
 for R in (512, 1024, 2048):
