@@ -300,12 +300,26 @@ def test_timed_execution_reports_every_launch():
     # (the last pass stores natural order itself at this size: no interleave launch)
     assert d["launch_kind"] == ["tree", "pass", "pass"]
     # asynchronous profiling: events for 3 back-to-back executions, one read
-    plan.profile_start(3)
+    plan.profile_start(3, pifft.PROFILE_ALL)
     for _ in range(5):  # only the first 3 are recorded
         plan.execute_device(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
-    used, sums = plan.profile_read()
-    assert used == 3 and len(sums) == d["num_launches"] and all(m > 0 for m in sums)
+    used, sums, cnt = plan.profile_read()
+    assert used == 3 and len(sums) == d["num_launches"] and all(m > 0 for m in sums) and cnt == [3, 3, 3]
     assert plan.profile_read()[0] == 0
+    # in-context sampling: odd executions time launch (k/2) mod 3 -> 2 samples each in 12
+    plan.profile_start(12, pifft.PROFILE_SAMPLED)
+    for _ in range(12):
+        plan.execute_device(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
+    used, sums, cnt = plan.profile_read()
+    assert used == 12 and cnt == [2, 2, 2] and all(m > 0 for m in sums)
+    with pytest.raises(pifft.PifftError, match="profile mode"):
+        plan.profile_start(3, 7)
+    torch.cuda.synchronize()
+    # the profiled executions compute the same transform
+    want = y.clone()
+    plan.execute_device(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y, want)
 
 
 def test_device_errors():
