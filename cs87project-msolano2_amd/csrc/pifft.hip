@@ -150,6 +150,7 @@ struct pifft_plan {
     bool natural = true;
     bool bitrev = false;  // PIFFT_OUT_BITREV
     bool ilv = false;     // the last pass stores natural order itself (PassArgs::ilv_log)
+    bool wil = false;     // worker-interleaved layout (PassArgs::wil, MODE | 8 passes)
     bool separate_tree = false;  // PIFFT_SEPARATE_TREE: never fuse the tree into a pass
     std::vector<Step> steps;
     int tree_steps = 0, npasses = 0;
@@ -585,10 +586,38 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // stays in the Infinity Cache -- PIFFT_FUSE_ALL_MAX_MIB of input
     // (measured, profiles/r02_fuse_all.log: no consistent win, off by default)
     const uint64_t in_mib = ((uint64_t)p->batch * p->n * esz) >> 20;
-    const bool fuse_all = p->nq > 1 && in_mib < (uint64_t)env_int("PIFFT_FUSE_ALL_MAX_MIB", 0);
+    // All P <= 16 workers of a natural-order plan on this GPU, with a
+    // multi-pass local FFT: the worker-interleaved layout (PassArgs::wil).
+    // The tree's one launch writes z_q[i] at i P + q, every pass reads and
+    // writes rows holding all workers' values side by side, and the last pass
+    // stores worker q at slot bitrev(q) -- the natural-order result, without
+    // an interleave launch or scattered 16-B stores.  PIFFT_WORKER_IL=0: the
+    // slice-major layout (+ interleave launch or natural-order store).
+    const bool wil_ok = p->natural && p->P > 1 && p->nq == p->P && p->lp <= 4 && env_int("PIFFT_WORKER_IL", 1) &&
+                        env_int("PIFFT_CHUNK_MIB", 0) <= 0;
+    const bool fuse_all = !wil_ok && p->nq > 1 && in_mib < (uint64_t)env_int("PIFFT_FUSE_ALL_MAX_MIB", 0);
     const bool may_fuse = p->P > 1 && (p->nq == 1 || fuse_all) && p->lp <= 4 && !p->separate_tree &&
                           env_int("PIFFT_FUSE_TREE", 1);
     if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0)) return -1;
+    if (wil_ok && passes.size() > 1) {
+        // the same radices, every pass a worker-interleaved MODE 2 (| 8)
+        // pass at the C of a MODE 2 pass whose lines run over all workers
+        std::vector<PassChoice> w = passes;
+        bool ok = true;
+        for (auto& pc : w) {
+            const uint64_t lines = p->m / (uint64_t)pc.R;
+            pc.C = pick_lines(p->prec, pc.R, lines << p->lp, ntrans * lines,
+                              p->prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", 2);
+            pc.mode = 2 | 8;
+            pc.vpt = 16;
+            pc.h = 1;
+            ok = ok && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts) != nullptr;
+        }
+        if (ok) {
+            passes = w;
+            p->wil = true;
+        }
+    }
     if (p->bitrev && !passes.empty()) {
         // the last pass stores in bit-reversed order: its MODE | 4 twin, at
         // the planned C or the widest instantiated one below it
@@ -615,7 +644,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // PIFFT_ILV: -1 this rule, 0 never, 1 always (where it applies).
     {
         const int force = env_int("PIFFT_ILV", -1);
-        const bool ok = p->natural && p->P > 1 && p->nq == p->P && !passes.empty() &&
+        const bool ok = p->natural && p->P > 1 && p->nq == p->P && !passes.empty() && !p->wil &&
                         env_int("PIFFT_CHUNK_MIB", 0) <= 0;
         bool on = ok && force == 1;
         if (ok && force < 0) {
@@ -657,7 +686,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         tw_r[i] = (found != (size_t)-1) ? found : tb.roots(passes[i].R, passes[i].R, 1);
     }
     TwoLevel pass2;
-    if (passes.size() > 1) pass2 = two_level(tb, p->m);
+    if (passes.size() > 1) pass2 = two_level(tb, p->m);  // (every worker-interleaved plan has >= 2 passes)
     tb.align();
     p->tw_bytes = tb.blob.size() ? tb.blob.size() : 256;
     if (!dry) {
@@ -725,10 +754,15 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
         if (nl > 1) p->bytes_ta = (size_t)p->batch * p->n * esz;
         // the stand-alone tree (pifft_tree_device) reads d_in and writes d_seg
+        // (slice-major, always)
         for (Step t : e.steps) {
             if (t.src == -1) t.src = BUF_IN;
             if (t.dst == -2) t.dst = BUF_OUT;
             p->tree_only.push_back(t);
+        }
+        if (p->wil) {  // one launch over all workers (lp <= 4): the passes' interleaved layout
+            e.steps.back().ta.wil_out = 1;
+            e.steps.back().ta.out_bstride = p->n;
         }
         if (!fused) {
             p->tree_steps = (int)e.steps.size();
@@ -776,6 +810,11 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.rd_virt = s.pa.wr_virt = 0;
         s.pa.in_log_es = s.pa.log_lb;
         s.pa.out_log_ns = s.pa.log_ns;
+        if (p->wil) {
+            s.pa.wil = (uint32_t)p->lp;
+            s.pa.wbrev = (i + 1 == passes.size()) ? 1u : 0u;  // the last pass: natural order
+            s.pa.in_bstride = s.pa.out_bstride = p->n;          // a transform's P interleaved workers
+        }
         if (p->ilv && i + 1 == passes.size()) {
             s.pa.ilv_log = (uint32_t)p->lp;
             s.pa.out_bstride = p->n;
@@ -804,7 +843,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         chain.push_back(e);
     }
     if (chunk_last_two(p, passes, chain, dry)) return -1;
-    if (p->natural && p->P > 1 && !p->ilv) {
+    if (p->natural && p->P > 1 && !p->ilv && !p->wil) {
         Step s;
         s.kind = STEP_INTERLEAVE;
         s.fn = interleave_fn(p->prec, p->lp, p->n);
@@ -847,7 +886,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     uint64_t w_tr = M;  // elements per transform in W
     const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));
     const uint64_t w_min = (uint64_t)env_int("PIFFT_W_PAD_MIN_MIB", 2048) << 20;
-    if (w_pad && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
+    if (w_pad && !p->wil && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
         for (size_t i = 0; i + 1 < p->steps.size(); i++) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
@@ -1255,6 +1294,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     info->out_elems = out_elems(p);
     info->workspace_bytes = p->bytes_w + p->bytes_ta + p->bytes_tb + p->bytes_ch + p->tw_bytes;
     info->chunk_pairs = p->chunk_pairs;
+    info->layout = (p->wil ? 1 : 0) | (p->ilv ? 2 : 0);
     info->num_launches = (int)p->steps.size();
     info->num_passes = p->npasses;
     info->tree_launches = p->tree_steps;

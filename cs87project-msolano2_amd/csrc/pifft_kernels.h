@@ -468,6 +468,15 @@ struct PassArgs {
     // or slow (pass 3 1.58 vs 1.70-1.86 ms) by how the two allocations
     // happened to line up (tools/probe_place.py, tools/probe_pair.hip).
     uint32_t in_pad, out_pad, out_pad_log;
+    // Worker-interleaved layout (MODE | 8, all P <= 16 workers of a natural-
+    // order plan on one GPU): worker q's element e of transform bt sits at
+    // bt bstride + e 2^wil + q, and launch line L = (j << wil) + q within a
+    // transform -- line j of every worker back to back, so a tile's rows hold
+    // all workers' values side by side (row segments 2^wil times wider) and
+    // the last pass, storing worker q at slot bitrev(q) (wbrev), writes the
+    // natural-order result bitrev(q) + P k directly: no interleave launch and
+    // no scattered 16-B stores.
+    uint32_t wil, wbrev;
 };
 
 // The line map is compiled only into the chunked-pair instances (NTS 2 / 3):
@@ -731,6 +740,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     // store path cost 5-15 % on every pass (tools/ab.sh).
     constexpr int BM = MODE & 3;
     constexpr bool BREV = (MODE & 4) != 0;
+    constexpr bool WIL = (MODE & 8) != 0;  // worker-interleaved layout (PassArgs::wil)
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
@@ -745,8 +755,12 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     // Ns = 1 for a first pass: compile-time values measured 2 % slower there)
     const uint32_t log_lb = a.log_lb;
     const uint32_t log_ns = a.log_ns;
-    const uint64_t lb_mask = (1ull << log_lb) - 1;
     const uint64_t ns_mask = (1ull << log_ns) - 1;
+    // lines per transform (= element stride of a line): 2^log_lb, or with the
+    // worker-interleaved layout 2^(log_lb + wil) launch lines L = (j << wil) + q
+    const uint32_t wil = WIL ? a.wil : 0u;
+    const uint32_t lbi = log_lb + wil;
+    const uint64_t lb_mask = (1ull << lbi) - 1;
 
     // MODE 2: the inter-pass twiddle factors depend only on (line, b); their
     // two-level table entries are fetched with the data, not after it (a
@@ -764,7 +778,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int u = 0; u < U; u++) {
             int c, b;
             St::map(tid, u, c, b);
-            const uint64_t jm = global_line<NTS>(a, (tile * C + c) & lb_mask) & ns_mask;
+            const uint64_t jm = (global_line<NTS>(a, (tile * C + c) & lb_mask) >> wil) & ns_mask;
             const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
             if (!share_anc || u == 0) {
                 tw_pre[4 * u + 0] = tlo[e0 & hmask];
@@ -786,10 +800,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             constexpr bool CL = clamp_loads<T>();
             const bool ok = CL || tile * C + c < a.nlines;
             const uint64_t line = (!CL || tile * C + c < a.nlines) ? tile * C + c : a.nlines - 1;
-            const uint64_t bt = line >> log_lb, l = line & lb_mask;
+            const uint64_t bt = line >> lbi, l = line & lb_mask;
             constexpr bool CHUNK = NTS == 2 || NTS == 3;
             const uint64_t j = (CHUNK && a.rd_virt) ? l : global_line<NTS>(a, l);
-            const uint32_t les = CHUNK ? a.in_log_es : log_lb;
+            const uint32_t les = CHUNK ? a.in_log_es : lbi;
             // MODE 3: transform bt is worker (bt mod nq) of batch bt / nq, and
             // the leaves come from that batch's input
             const uint64_t bin = BM == 3 ? (bt >> a.log_nq) : bt;
@@ -922,12 +936,21 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
-                const uint64_t bt = line >> log_lb, l = line & lb_mask;
+                const uint64_t bt = line >> lbi, l = line & lb_mask;
                 constexpr bool CHUNK = NTS == 2 || NTS == 3;
-                const uint64_t j = (CHUNK && a.wr_virt) ? l : global_line<NTS>(a, l);
+                const uint64_t lj = (CHUNK && a.wr_virt) ? l : global_line<NTS>(a, l);
+                const uint64_t j = lj >> wil;  // the worker's own line
                 const uint32_t lns = CHUNK ? a.out_log_ns : (uint32_t)log_ns;
                 const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
-                if constexpr (!BREV) {
+                if constexpr (WIL) {
+                    // worker q at slot q (or bitrev(q): the natural-order result)
+                    const uint32_t wq = (uint32_t)(lj & ((1ull << wil) - 1));
+                    const uint64_t slot = a.wbrev ? (uint64_t)(__builtin_bitreverse32(wq) >> (32 - wil)) : wq;
+                    C2* dst = out + bt * a.out_bstride + (pos << wil) + slot;
+                    const uint32_t ks = lns + wil;
+#pragma unroll
+                    for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << ks), v[u * q + k]);
+                } else if constexpr (!BREV) {
                     // (ilv_log = 0: dst = out + bt out_bstride + pos + k NB 2^lns)
                     const uint32_t il = a.ilv_log;
                     const uint64_t rq = il ? (uint64_t)(__builtin_bitreverse32((uint32_t)bt) >> (32 - il)) : 0;
@@ -1091,6 +1114,9 @@ struct TreeArgs {
     uint64_t total;         // transforms * (N >> L)
     uint32_t log_n, log_p, t0;
     uint32_t q0, nq;        // workers [q0, q0+nq)
+    // the single launch of an all-worker tree writes the worker-interleaved
+    // layout of the passes (PassArgs::wil): z_q[i] at i 2^log_p + q
+    uint32_t wil_out;
 };
 
 template <typename T, int L>
@@ -1117,6 +1143,14 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
 #pragma unroll
     for (int m = 0; m < V; m++) v[m] = src[(uint64_t)m << log_d];
     tree_levels<T, L>(v, a.tw, i, log_d, a.t0, blk0, log_w, q0, q1);
+    if (a.wil_out) {
+        // (one launch over all P = 2^L workers: base = 0, D = N / P, worker m's
+        // element i is position i + m D) -- one 2^L-value run per thread
+        C2* dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (i << L);
+#pragma unroll
+        for (int m = 0; m < V; m++) dst[m] = v[m];
+        continue;
+    }
     C2* dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (int64_t)(base + i) + a.out_shift;
 #pragma unroll
     for (int m = 0; m < V; m++) {

@@ -54,6 +54,7 @@ class PlanInfo(ctypes.Structure):
         ("launch_kind", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("launch_fn", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("vpt", ctypes.c_int32 * 8),
+        ("layout", ctypes.c_int32),
     ]
 
 
@@ -245,6 +246,7 @@ def describe_info(i: PlanInfo) -> dict:
         "chunk_pairs": i.chunk_pairs,
         "launch_fn": list(i.launch_fn[: min(nl, MAX_LAUNCH_INFO)]),
         "vpt": list(i.vpt[: i.num_passes]),
+        "worker_interleaved": bool(i.layout & 1), "natural_store": bool(i.layout & 2),
     }
 
 

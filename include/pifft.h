@@ -96,6 +96,11 @@ typedef struct pifft_plan_info {
                                   of first use) -- what rocprof aggregates per kernel */
     int32_t vpt[8];          /* complex values per thread of each pass (16; 8 for single
                                 passes too small to fill the GPU at 16)            */
+    int32_t layout;          /* bit 0: worker-interleaved passes (all P <= 16 workers of a
+                                natural-order plan: the last pass writes natural order);
+                                bit 1: the last pass stores natural order from the
+                                slice-major layout (small outputs); neither: slice-major
+                                passes (+ an interleave launch for natural order)   */
 } pifft_plan_info;
 
 /* Last error message of the calling thread ("" if none). */

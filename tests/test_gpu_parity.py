@@ -709,6 +709,36 @@ def test_chunked_pass_pair_config4_bitwise(monkeypatch):
     assert torch.equal(torch.view_as_real(a), torch.view_as_real(b))
 
 
+# ---------------------------------------- worker-interleaved layout (wil) ---
+@pytest.mark.parametrize("suf,logn,P,batch", [("f64", 20, 8, 1), ("f64", 21, 2, 2), ("f32", 20, 8, 3),
+                                              ("f64", 18, 16, 1), ("f32", 22, 4, 1), ("f64", 17, 8, 2),
+                                              ("f64", 24, 8, 1), ("f32", 15, 2, 5)])
+def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypatch):
+    """All-worker natural-order plans on the worker-interleaved layout (tree
+    writing z_q[i] at i P + q, MODE 10 passes, the last one storing worker q
+    at slot bitrev(q)) equal the slice-major plans (PIFFT_WORKER_IL=0: the
+    same per-line arithmetic, then the interleave or the natural-order store)
+    value for value, and the oracle within tolerance."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn * 3 + P)
+    d_in = dev(x)
+    st = torch.cuda.current_stream()
+    wil = pifft.Plan(n, P, batch, PREC[suf])
+    assert wil.describe()["worker_interleaved"] and "interleave" not in wil.describe()["launch_kind"]
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")
+    sm = pifft.Plan(n, P, batch, PREC[suf])
+    assert not sm.describe()["worker_interleaved"]
+    a = torch.empty_like(d_in)
+    b = torch.empty_like(d_in)
+    wil.execute_device(d_in.data_ptr(), a.data_ptr(), st)
+    sm.execute_device(d_in.data_ptr(), b.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    got = a.cpu().numpy().reshape(batch, n)
+    for bt in range(batch):
+        assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
+
+
 # ------------------------------------------------ the final exchange (8e) ---
 @pytest.mark.parametrize("suf,logn,P,per,batch", [("f64", 20, 8, 1, 1), ("f32", 18, 8, 2, 3), ("f64", 16, 4, 1, 2),
                                                   ("f64", 12, 64, 16, 1)])

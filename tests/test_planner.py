@@ -22,11 +22,15 @@ def test_config2_2e20_fp64_eight_workers_one_gpu():
     assert d["local_n"] == 1 << 17 and d["out_elems"] == 1 << 20
 
 
-def test_natural_store_rule():
+def test_natural_store_rule(monkeypatch):
     """The planner's rule for the last pass storing natural order itself
-    (pifft.hip build_plan, PIFFT_ILV): small outputs with enough tiles; the
-    separate interleave launch above 64 MiB (fp64) / 16 MiB (fp32) and for
-    tiny plans; batched single-pass plans up to 128 MiB."""
+    (pifft.hip build_plan, PIFFT_ILV) on the slice-major layout (multi-pass
+    all-worker plans use the worker-interleaved layout by default, off here):
+    small outputs with enough tiles; the separate interleave launch above
+    64 MiB (fp64) / 16 MiB (fp32) and for tiny plans; batched single-pass
+    plans up to 128 MiB."""
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")
+
     def kinds(n, P, b, prec):
         return pifft.dry_run(n, P, b, prec)["launch_kind"]
     assert kinds(1 << 22, 8, 1, F64)[-1] == "pass"
@@ -131,11 +135,13 @@ def test_dry_run_validation():
 
 
 @pytest.mark.parametrize("P", [1, 8])
-def test_bitrev_output_needs_no_interleave(P):
+def test_bitrev_output_needs_no_interleave(P, monkeypatch):
     """PIFFT_OUT_BITREV (the reference's scratch order): the
     whole transform on one GPU skips the interleave launch."""
-    # (2^23: above the size where natural plans store natural order from their
-    # last pass, so the natural plan has the interleave launch)
+    # (2^23 on the slice-major layout: above the size where natural plans
+    # store natural order from their last pass, so the natural plan has the
+    # interleave launch)
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")
     nat = pifft.dry_run(1 << 23, P, 1, F64)
     d = pifft.dry_run(1 << 23, P, 1, F64, flags=pifft.OUT_BITREV)
     assert "interleave" not in d["launch_kind"]
@@ -194,3 +200,23 @@ def test_separate_tree_flag():
     assert sep["num_passes"] == fused["num_passes"]
     with pytest.raises(pifft.PifftError, match="unknown flags"):
         pifft.dry_run(n, P, 1, F64, first=0, count=1, flags=8)
+
+
+def test_worker_interleaved_layout(monkeypatch):
+    """All P <= 16 workers of a natural-order plan with a multi-pass local FFT
+    use the worker-interleaved layout: tree + passes, no interleave launch and
+    no scattered natural-order store; PIFFT_WORKER_IL=0 restores the
+    slice-major layout.  Single-pass local FFTs, P > 16 and worker ranges keep
+    the slice-major layout."""
+    d = pifft.dry_run(1 << 20, 8, 1, F64)
+    assert d["worker_interleaved"] and not d["natural_store"] and d["launch_kind"] == ["tree", "pass", "pass"]
+    big = pifft.dry_run(1 << 28, 8, 1, F64)
+    assert big["worker_interleaved"] and "interleave" not in big["launch_kind"]
+    assert not pifft.dry_run(1 << 16, 8, 1, F64)["worker_interleaved"]          # single-pass local FFT
+    assert not pifft.dry_run(1 << 20, 32, 1, F64)["worker_interleaved"]         # two tree launches
+    assert not pifft.dry_run(1 << 20, 8, 1, F64, first=0, count=4)["worker_interleaved"]
+    assert not pifft.dry_run(1 << 20, 1, 1, F64)["worker_interleaved"]
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")
+    d0 = pifft.dry_run(1 << 20, 8, 1, F64)
+    assert not d0["worker_interleaved"] and d0["natural_store"]
+    assert pifft.dry_run(1 << 28, 8, 1, F64)["launch_kind"][-1] == "interleave"

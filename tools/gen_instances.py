@@ -4,6 +4,7 @@ spread over NPART translation units (compiled in parallel).
 
 Rules: NT = C*R/VPT threads (VPT = 16 values per thread) <= 1024; LDS = C*(R + R/16 + 1)*sizeof(T)
 <= 160 KiB.  MODE 0 single pass (any C); MODE 1/2 strided passes (C >= 4);
+MODE 10 = MODE 2 on the worker-interleaved layout (all-worker plans).
 MODE 3 = MODE 1 with the tree fused in, LP = log2 P in 1..4, at the planner's
 tile (8192 elements, both precisions) and C = 4.  MODE 4 / 6 = MODE 0 / 2
 storing in bit-reversed order (the last pass of a PIFFT_OUT_BITREV plan), for
@@ -34,6 +35,10 @@ for T, prec, esz, tile, vpt in (("double", 64, 8, 8192, 16), ("float", 32, 4, 16
                     items.append(f"PK({T}, {prec}, {R}, {C}, 2, {nts}, 0),")
                     if C <= max(4, tile // R):
                         items.append(f"PK({T}, {prec}, {R}, {C}, 6, {nts}, 0),")
+                        # MODE 10 = 2 | 8: the worker-interleaved layout of
+                        # all-worker plans (multi-pass local FFTs: R <= 1024)
+                        if R <= 1024:
+                            items.append(f"PK({T}, {prec}, {R}, {C}, 10, {nts}, 0),")
                     # chunked pass pairs (nt loads only / nt stores only) at
                     # the planner's tile
                     # (and the 4096-value tile of fp64 R <= 256 later passes)
