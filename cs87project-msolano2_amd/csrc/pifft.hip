@@ -611,6 +611,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
             pc.mode = 2 | 8;
             pc.vpt = 16;
             pc.h = 1;
+            // tuning: at least this many lines per workgroup (e.g. P, so a
+            // row holds every worker's value), if instantiated
+            const int cmin = env_int("PIFFT_WIL_CMIN", 0);
+            if (cmin > pc.C && find_pass(p->prec, pc.R, cmin, pc.mode, pc.nts)) pc.C = cmin;
             ok = ok && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts) != nullptr;
         }
         if (ok) {
@@ -761,8 +765,15 @@ int build_plan(pifft_plan* p, bool dry = false) {
             p->tree_only.push_back(t);
         }
         if (p->wil) {  // one launch over all workers (lp <= 4): the passes' interleaved layout
-            e.steps.back().ta.wil_out = 1;
-            e.steps.back().ta.out_bstride = p->n;
+            static const void* tw64[5] = {nullptr, (const void*)&k_tree_wil<double, 1>, (const void*)&k_tree_wil<double, 2>,
+                                          (const void*)&k_tree_wil<double, 3>, (const void*)&k_tree_wil<double, 4>};
+            static const void* tw32[5] = {nullptr, (const void*)&k_tree_wil<float, 1>, (const void*)&k_tree_wil<float, 2>,
+                                          (const void*)&k_tree_wil<float, 3>, (const void*)&k_tree_wil<float, 4>};
+            Step& t = e.steps.back();
+            t.fn = p->prec == 64 ? tw64[p->lp] : tw32[p->lp];
+            t.ta.out_bstride = p->n;
+            t.lds = (size_t)tree_wil_pad(256u << p->lp) * esz;
+            if (t.lds > 65536 && !dry) (void)hipFuncSetAttribute(t.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)t.lds);
         }
         if (!fused) {
             p->tree_steps = (int)e.steps.size();
@@ -1003,7 +1014,7 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             a.in = src;
             a.out = dst;
             void* args[] = {&a};
-            e = go(args, 0);
+            e = go(args, s.lds);
             break;
         }
         case STEP_INTERLEAVE: {

@@ -1114,9 +1114,6 @@ struct TreeArgs {
     uint64_t total;         // transforms * (N >> L)
     uint32_t log_n, log_p, t0;
     uint32_t q0, nq;        // workers [q0, q0+nq)
-    // the single launch of an all-worker tree writes the worker-interleaved
-    // layout of the passes (PassArgs::wil): z_q[i] at i 2^log_p + q
-    uint32_t wil_out;
 };
 
 template <typename T, int L>
@@ -1143,14 +1140,6 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
 #pragma unroll
     for (int m = 0; m < V; m++) v[m] = src[(uint64_t)m << log_d];
     tree_levels<T, L>(v, a.tw, i, log_d, a.t0, blk0, log_w, q0, q1);
-    if (a.wil_out) {
-        // (one launch over all P = 2^L workers: base = 0, D = N / P, worker m's
-        // element i is position i + m D) -- one 2^L-value run per thread
-        C2* dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (i << L);
-#pragma unroll
-        for (int m = 0; m < V; m++) dst[m] = v[m];
-        continue;
-    }
     C2* dst = static_cast<C2*>(a.out) + bt * a.out_bstride + (int64_t)(base + i) + a.out_shift;
 #pragma unroll
     for (int m = 0; m < V; m++) {
@@ -1158,6 +1147,47 @@ __global__ __launch_bounds__(256) void k_tree(TreeArgs a) {
         if (wm < q1 && wm + (1ull << log_w) > q0) dst[(uint64_t)m << log_d] = v[m];
     }
     }  // grid-stride
+}
+
+// The single launch of an all-worker tree (t0 = 0, all P = 2^L workers)
+// writing the worker-interleaved layout of the passes (PassArgs::wil):
+// z_q[i] at bt out_bstride + i P + q.  A block's 256 threads own 256
+// consecutive i -- one contiguous run of 256 P outputs (M = N / P >= 256) --
+// staged through LDS (one pad value per 8) so that every store instruction
+// writes 64 consecutive values instead of 64 pieces P values apart.
+// Dynamic LDS: 256 P (9/8) values.
+__host__ __device__ constexpr uint32_t tree_wil_pad(uint32_t idx) { return idx + (idx >> 3); }
+template <typename T, int L>
+__global__ __launch_bounds__(256) void k_tree_wil(TreeArgs a) {
+    using C2 = cx<T>;
+    constexpr int V = 1 << L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
+    C2* stage = reinterpret_cast<C2*>(pifft_smem);
+    const uint32_t log_d = a.log_n - L;  // 2^log_d = M threads per transform
+    const uint64_t nblk = (a.total + 255) / 256;
+    // (block-uniform loop: every thread of a block reaches the barriers)
+    for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint64_t g0 = blk * 256, gid = g0 + threadIdx.x;
+        const uint64_t g = gid < a.total ? gid : a.total - 1;
+        const uint64_t bt = g >> log_d, i = g & ((1ull << log_d) - 1);
+        const C2* src = static_cast<const C2*>(a.in) + bt * a.in_bstride + i;
+        C2 v[V];
+#pragma unroll
+        for (int m = 0; m < V; m++) v[m] = src[(uint64_t)m << log_d];
+        tree_levels<T, L>(v, a.tw, i, log_d, 0, 0, 0, 0, V);
+        __syncthreads();  // the previous round's reads of `stage` are done
+#pragma unroll
+        for (int m = 0; m < V; m++) stage[tree_wil_pad(threadIdx.x * V + m)] = v[m];
+        __syncthreads();
+        const uint64_t b0 = g0 >> log_d, i0 = g0 & ((1ull << log_d) - 1);
+        C2* dst = static_cast<C2*>(a.out) + b0 * a.out_bstride + (i0 << L);
+        const uint64_t nvalid = (a.total - g0 < 256 ? a.total - g0 : 256) * V;
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+            const uint32_t idx = (uint32_t)k * 256 + threadIdx.x;
+            if (idx < nvalid) dst[idx] = stage[tree_wil_pad(idx)];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -711,8 +711,8 @@ def test_chunked_pass_pair_config4_bitwise(monkeypatch):
 
 # ---------------------------------------- worker-interleaved layout (wil) ---
 @pytest.mark.parametrize("suf,logn,P,batch", [("f64", 20, 8, 1), ("f64", 21, 2, 2), ("f32", 20, 8, 3),
-                                              ("f64", 18, 16, 1), ("f32", 22, 4, 1), ("f64", 17, 8, 2),
-                                              ("f64", 24, 8, 1), ("f32", 15, 2, 5)])
+                                              ("f64", 19, 16, 1), ("f32", 22, 4, 1), ("f64", 18, 8, 2),
+                                              ("f64", 24, 8, 1), ("f32", 16, 2, 5), ("f32", 23, 16, 1)])
 def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypatch):
     """All-worker natural-order plans on the worker-interleaved layout (tree
     writing z_q[i] at i P + q, MODE 10 passes, the last one storing worker q
