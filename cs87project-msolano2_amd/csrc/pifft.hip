@@ -63,6 +63,12 @@ int env_int(const char* name, int dflt) {
     return (s && *s) ? atoi(s) : dflt;
 }
 
+// Timing events only time (pifft_execute_device_timed, pifft_profile_*,
+// pifft_execute_group's stage timers): no system-scope fence when they are
+// recorded, so a timed kernel does not pay an L2 write-back at its end (a
+// bound stop event otherwise made C3's 44-us kernel read 50 us)
+constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
+
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 
 // 1-D grid for a grid-stride kernel of `total` items at 256 threads/block:
@@ -613,7 +619,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
             pc.h = 1;
             // tuning: at least this many lines per workgroup (e.g. P, so a
             // row holds every worker's value), if instantiated
-            const int cmin = env_int("PIFFT_WIL_CMIN", 0);
+            // (default P: 8 workers at C = 8 instead of 4 -- C2 35 -> 32 us,
+            // fp32 2^20 P = 8 25 -> 24 us, 2^28 P = 8 unchanged at C = 16;
+            // profiles/r03_worker_interleaved.log)
+            const int cmin = env_int("PIFFT_WIL_CMIN", (int)p->P);
             if (cmin > pc.C && find_pass(p->prec, pc.R, cmin, pc.mode, pc.nts)) pc.C = cmin;
             ok = ok && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts) != nullptr;
         }
@@ -927,7 +936,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     if (p->bytes_ch) HIPCHK(hipMalloc(&p->buf[BUF_CH], p->bytes_ch));
     HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->ev.resize(2 * p->steps.size());
-    for (auto& e : p->ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : p->ev) HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
     return 0;
 }
 
@@ -1368,7 +1377,7 @@ int pifft_profile_start(pifft_plan* p, int steps, int mode) {
     const size_t need = (size_t)steps * 2 * (mode == PIFFT_PROFILE_ALL ? p->steps.size() : 1);
     while (p->prof_ev.size() < need) {
         hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
         p->prof_ev.push_back(e);
     }
     p->prof_steps = steps;
