@@ -111,3 +111,36 @@ def test_random_large_plan_vs_oracle(suf, logn, P, first, count, batch, flags):
     FFTs, the natural-store and interleave rules, fused trees), vs the oracle
     on 16 host threads."""
     test_random_plan_vs_oracle(suf, logn, P, first, count, batch, flags)
+
+
+def _wil_cases(count=16, seed=20261018):
+    """Natural-order all-worker shapes with P <= 16 and a multi-pass local FFT
+    (M = N/P >= 2^15): the worker-interleaved layout's domain."""
+    rng = random.Random(seed)
+    out = []
+    while len(out) < count:
+        suf = rng.choice(["f32", "f64"])
+        lp = rng.randint(1, 4)
+        logn = rng.randint(15 + lp, 22)
+        batch = rng.choice([1, 1, 2, 3])
+        if (1 << logn) * batch > 1 << 22:
+            batch = 1
+        out.append((suf, logn, 1 << lp, batch))
+    return out
+
+
+@pytest.mark.parametrize("suf,logn,P,batch", _wil_cases())
+def test_random_worker_interleaved_plan_vs_oracle(suf, logn, P, batch):
+    """Seeded random shapes on the worker-interleaved layout (tree writing
+    z_q[i] at i P + q, MODE 10 passes, natural-order last pass) vs the oracle."""
+    n = 1 << logn
+    xs = [oracle.generate(n, DT[suf], seed=logn * 17 + P + b) for b in range(batch)]
+    plan = pifft.Plan(n, P, batch, PREC[suf])
+    assert plan.describe()["worker_interleaved"], plan.describe()
+    d_in = dev(np.concatenate(xs))
+    d_out = torch.empty(plan.info.out_elems, dtype=d_in.dtype, device="cuda")
+    plan.execute_device(d_in.data_ptr(), d_out.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().reshape(batch, n)
+    for b in range(batch):
+        assert_bins_close(got[b], oracle.fft(xs[b], P=1, nthreads=8), suf, n)
