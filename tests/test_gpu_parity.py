@@ -935,6 +935,7 @@ def test_fused_tree_all_workers(suf, logn, P, batch, monkeypatch):
     n = 1 << logn
     x = oracle.generate(n * batch, DT[suf], seed=logn + P)
     monkeypatch.setenv("PIFFT_FUSE_ALL_MAX_MIB", "100000")
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")  # (the worker-interleaved layout takes precedence)
     fused = pifft.Plan(n, P, batch, PREC[suf])
     monkeypatch.delenv("PIFFT_FUSE_ALL_MAX_MIB")
     plain = pifft.Plan(n, P, batch, PREC[suf])
