@@ -1025,6 +1025,7 @@ def test_natural_store_in_last_pass(suf, logn, P, batch, monkeypatch):
     batches, lines per transform below and above the tile's."""
     n = 1 << logn
     x = oracle.generate(n * batch, DT[suf], seed=logn * 3 + P + batch)
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")  # the slice-major layout's natural store
     monkeypatch.setenv("PIFFT_ILV", "1")
     ilv = pifft.Plan(n, P, batch, PREC[suf])
     monkeypatch.setenv("PIFFT_ILV", "0")
@@ -1058,6 +1059,7 @@ def test_padded_workspace_rows(suf, logn, P, first, count, batch, flags, pad, mo
     ranges, bit-reversed output) and an odd pad."""
     n = 1 << logn
     x = oracle.generate(n * batch, DT[suf], seed=logn + 7 * P + batch)
+    monkeypatch.setenv("PIFFT_WORKER_IL", "0")  # (worker-interleaved plans keep W unpadded)
     monkeypatch.setenv("PIFFT_W_PAD_MIN_MIB", "0")
     monkeypatch.setenv("PIFFT_W_PAD", str(pad))
     padded = pifft.Plan(n, P, batch, PREC[suf], first=first, count=count, flags=flags)
