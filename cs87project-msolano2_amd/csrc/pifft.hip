@@ -1370,6 +1370,64 @@ int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* str
     return 0;
 }
 
+int pifft_plan_tune_workspace(pifft_plan* p, const void* d_in, void* d_out, void* stream, int tries,
+                              float* best_ms) {
+    if (check_buffers(p, d_in, d_out)) return -1;
+    if (tries < 1) return fail("tries must be >= 1");
+    DeviceGuard g(p->device);
+    hipStream_t st = (hipStream_t)stream;
+    if (!p->buf[BUF_W] || tries == 1) {  // nothing to place
+        if (best_ms) *best_ms = 0.0f;
+        return 0;
+    }
+    hipEvent_t e[2];
+    HIPCHK(hipEventCreateWithFlags(&e[0], kTimingEventFlags));
+    if (hipEventCreateWithFlags(&e[1], kTimingEventFlags) != hipSuccess) {
+        (void)hipEventDestroy(e[0]);
+        return fail("hipEventCreate failed");
+    }
+    // mean of 3 executions after one warm-up, with the plan's current workspace
+    auto timed = [&](float& ms) -> int {
+        if (launch_steps(p, d_in, d_out, st, nullptr)) return -1;
+        HIPCHK(hipEventRecord(e[0], st));
+        for (int r = 0; r < 3; r++)
+            if (launch_steps(p, d_in, d_out, st, nullptr)) return -1;
+        HIPCHK(hipEventRecord(e[1], st));
+        HIPCHK(hipEventSynchronize(e[1]));
+        HIPCHK(hipEventElapsedTime(&ms, e[0], e[1]));
+        ms /= 3.0f;
+        return 0;
+    };
+    int rc = 0;
+    float best = 0.0f;
+    if (timed(best)) rc = -1;
+    for (int t = 1; t < tries && rc == 0; t++) {
+        void* keep = p->buf[BUF_W];
+        void* fresh = nullptr;
+        if (hipMalloc(&fresh, p->bytes_w) != hipSuccess) {
+            (void)hipGetLastError();
+            break;  // no room for a second workspace: keep the first
+        }
+        p->buf[BUF_W] = fresh;
+        float ms = 0.0f;
+        if (timed(ms)) {
+            rc = -1;
+        } else if (ms < best) {
+            best = ms;
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(keep);
+            continue;
+        }
+        (void)hipStreamSynchronize(st);
+        p->buf[BUF_W] = keep;
+        (void)hipFree(fresh);
+    }
+    (void)hipEventDestroy(e[0]);
+    (void)hipEventDestroy(e[1]);
+    if (best_ms) *best_ms = best;
+    return rc;
+}
+
 int pifft_profile_start(pifft_plan* p, int steps, int mode) {
     if (!p || steps < 0) return fail("bad arguments");
     if (mode != PIFFT_PROFILE_ALL && mode != PIFFT_PROFILE_SAMPLED) return fail("unknown profile mode %d", mode);

@@ -86,6 +86,7 @@ _SIGS = {
                                                ctypes.c_int, _P]),
     "pifft_tree_device": (ctypes.c_int, [_P, _P, _P, _P]),
     "pifft_profile_start": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int]),
+    "pifft_plan_tune_workspace": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int),
                                           ctypes.c_int]),
     "pifft_allgather": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_P),
@@ -195,6 +196,14 @@ class Plan:
         _check(lib().pifft_execute_device_timed(self._h, d_in, d_out, _stream(stream), buf, n),
                "pifft_execute_device_timed")
         return list(buf[:n])
+
+    def tune_workspace(self, d_in: int, d_out: int, stream=None, tries: int = 4) -> float:
+        """pifft_plan_tune_workspace: keep the fastest of `tries` workspace
+        placements for this (d_in, d_out); returns its mean execution ms."""
+        ms = ctypes.c_float()
+        _check(lib().pifft_plan_tune_workspace(self._h, d_in, d_out, _stream(stream), tries, ctypes.byref(ms)),
+               "pifft_plan_tune_workspace")
+        return ms.value
 
     def profile_start(self, steps: int, mode: int = 1) -> None:
         """mode PROFILE_SAMPLED (default; in-context) or PROFILE_ALL (isolated)."""

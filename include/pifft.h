@@ -157,6 +157,19 @@ int pifft_execute_device(pifft_plan* plan, const void* d_in, void* d_out, void* 
 int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, void* stream,
                                float* launch_ms, int max_launches);
 
+/* Workspace placement tuning (optional, like a measuring planner): the plan's
+ * ping-pong workspace W and the caller's d_out are read and written at the
+ * same row offsets by the later passes, and whether their physical pages
+ * collide in the DRAM banks depends on where each allocation lands (C4 passes
+ * 2 + 3: 2.92 ms in the fast state, 3.13-3.5 ms in the slow one; DESIGN.md
+ * section 4).  This call times the plan on (d_in, d_out) with its current W,
+ * then with up to tries - 1 freshly allocated ones, and keeps the fastest (one
+ * extra W at a time; stops early if it cannot allocate).  *best_ms (may be
+ * NULL) receives the kept workspace's mean execution time.  Synchronous.
+ * Results are unchanged; only timings move. */
+int pifft_plan_tune_workspace(pifft_plan* plan, const void* d_in, void* d_out, void* stream, int tries,
+                              float* best_ms);
+
 /* Asynchronous per-launch timing.  After pifft_profile_start(plan, steps,
  * mode) the next `steps` pifft_execute_device calls bind start/stop events to
  * launches (hipExtLaunchKernel: the dispatch's own timestamps, as rocprofv3
