@@ -335,6 +335,11 @@ class Job:
         pifft.generate_device(self.x.data_ptr(), n * batch_local, n, prec, seed=seed, first=b_first * n,
                               stream=self.stream)
         self.y = torch.empty(self.desc["out_elems"], dtype=cdt, device=self.dev)
+        # placement tuning before the warm-up (pifft_plan_tune_workspace: the
+        # fastest of 4 workspace allocations for this output; ~80 ms at 2^28,
+        # profiles/r03_workspace_tuning.log: C4 4.62-4.81 -> 4.59-4.62 ms)
+        self.tuned_ms = self.plan.tune_workspace(self.x.data_ptr(), self.y.data_ptr(), self.stream,
+                                                 int(os.environ.get("BENCH_W_TRIES", "4")))
 
     def step(self):
         self.plan.execute_device(self.x.data_ptr(), self.y.data_ptr(), self.stream)

@@ -322,6 +322,31 @@ def test_timed_execution_reports_every_launch():
     assert torch.equal(y, want)
 
 
+@pytest.mark.parametrize("suf,logn,P", [("f64", 22, 1), ("f32", 24, 1), ("f64", 21, 8)])
+def test_tune_workspace_keeps_results(suf, logn, P):
+    """pifft_plan_tune_workspace only re-places the plan's workspace: the
+    output is bitwise the untuned plan's; a plan without a workspace (single
+    pass) returns at once; tries < 1 is refused."""
+    n = 1 << logn
+    x = dev(oracle.generate(n, DT[suf], seed=logn))
+    st = torch.cuda.current_stream()
+    kw = dict(first=0, count=1, device=0) if P > 1 else {}
+    plan = pifft.Plan(n, P, 1, PREC[suf], **kw)
+    a = torch.empty(plan.info.out_elems, dtype=x.dtype, device="cuda")
+    plan.execute_device(x.data_ptr(), a.data_ptr(), st)
+    ms = plan.tune_workspace(x.data_ptr(), a.data_ptr(), st, 3)
+    assert ms > 0
+    b = torch.empty_like(a)
+    plan.execute_device(x.data_ptr(), b.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    single = pifft.Plan(4096, 1, 4, PREC[suf])
+    y = torch.empty(4 * 4096, dtype=x.dtype, device="cuda")
+    assert single.tune_workspace(x.data_ptr(), y.data_ptr(), st, 4) == 0.0
+    with pytest.raises(pifft.PifftError, match="tries"):
+        plan.tune_workspace(x.data_ptr(), a.data_ptr(), st, 0)
+
+
 def test_device_errors():
     plan = pifft.Plan(64, 2, 1, pifft.F64)
     x = torch.zeros(64, dtype=torch.complex128, device="cuda")
