@@ -1021,6 +1021,212 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 at 32 values per thread, packed (VPT 32): a 16384-value tile on 512
+// threads (two workgroups per CU), i.e. the bytes and row-segment widths of
+// the fp64 8192-value tile.  Each thread's butterflies u = 2m and 2m + 1 of a
+// stage travel together in one register pair per component (cx<f2>: .x the
+// even butterfly, .y the odd one), so their arithmetic is v_pk_add_f32 /
+// v_pk_mul_f32 on pairs -- the same operations in the same order as two
+// scalar butterflies (bitwise equal), with the register state of ONE fp64
+// butterfly instead of two interleaved fp32 ones (the scalar VPT-32 form wants
+// 174 VGPRs in MODE 2 and spills at 128).  Loads, stores and LDS exchanges
+// address each half with the VPT-32 Stage map of its own butterfly.
+// ---------------------------------------------------------------------------
+using f2 = float __attribute__((ext_vector_type(2)));
+
+template <int H>
+__device__ __forceinline__ void pk_put(cx<f2>& d, cx<float> s) {
+    if constexpr (H) {
+        d.re.y = s.re;
+        d.im.y = s.im;
+    } else {
+        d.re.x = s.re;
+        d.im.x = s.im;
+    }
+}
+template <int H>
+__device__ __forceinline__ cx<float> pk_get(const cx<f2>& d) {
+    if constexpr (H) return cx<float>{d.re.y, d.im.y};
+    else return cx<float>{d.re.x, d.im.x};
+}
+__device__ __forceinline__ cx<f2> pk_pair(cx<float> a, cx<float> b) {
+    cx<f2> r;
+    r.re = f2{a.re, b.re};
+    r.im = f2{a.im, b.im};
+    return r;
+}
+
+template <int R, int C, int MODE, int NTS, int S>
+__device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds, cx<f2>* vp, int tid, uint64_t tile,
+                                                   cx<float>* twp) {
+    using C1 = cx<float>;
+    using CP = cx<f2>;
+    constexpr int VPT = 32;
+    constexpr int BM = MODE & 3;
+    static_assert(BM == 1 || BM == 2, "packed VPT-32 passes: strided first / later passes");
+    static_assert((MODE & ~3) == 0 && (NTS == 0 || NTS == 1), "no bit-reversed, interleaved or chunked forms");
+    using St = Stage<R, C, BM, S, VPT>;
+    using Sh = PassShape<R, VPT>;
+    constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
+    static_assert(U % 2 == 0, "butterflies go in pairs");
+    constexpr LdsLayout LL = LdsPick<float, R, C, BM, VPT>::value;
+    const uint32_t log_lb = a.log_lb, log_ns = a.log_ns;
+    const uint64_t lb_mask = (1ull << log_lb) - 1, ns_mask = (1ull << log_ns) - 1;
+    constexpr bool share_anc = St::cfast && U > 1 && St::NT % C == 0;
+
+    if constexpr (St::first) {
+        if constexpr (BM == 2) {
+            const C1* tlo = static_cast<const C1*>(a.tw_lo);
+            const C1* thi = static_cast<const C1*>(a.tw_hi);
+            const uint64_t hmask = (1ull << a.tw_h) - 1;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                int c, b;
+                St::map(tid, u, c, b);
+                const uint64_t jm = (tile * C + c) & lb_mask & ns_mask;
+                const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
+                if (!share_anc || u == 0) {
+                    twp[4 * u + 0] = tlo[e0 & hmask];
+                    twp[4 * u + 1] = thi[e0 >> a.tw_h];
+                }
+                twp[4 * u + 2] = tlo[e1 & hmask];
+                twp[4 * u + 3] = thi[e1 >> a.tw_h];
+            }
+        }
+        // ---- inputs straight from HBM (all loads issued before any use) ----
+        const C1* __restrict__ in = static_cast<const C1*>(a.in);
+        static_for<0, U, 1>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            int c, b;
+            St::map(tid, u, c, b);
+            const uint64_t line = tile * C + c < a.nlines ? tile * C + c : a.nlines - 1;
+            const uint64_t bt = line >> log_lb, j = line & lb_mask;
+            const uint32_t les = log_lb;
+            if constexpr (BM == 2) {
+                const uint64_t rs = (1ull << les) + a.in_pad;
+                const C1* row = in + bt * a.in_bstride + j + (uint64_t)b * rs;
+#pragma unroll
+                for (int k = 0; k < q; k++)
+                    pk_put<u & 1>(vp[(u >> 1) * q + k], ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs));
+            } else {
+                const C1* src = in + bt * a.in_bstride + j + ((uint64_t)b << les);
+#pragma unroll
+                for (int k = 0; k < q; k++)
+                    pk_put<u & 1>(vp[(u >> 1) * q + k], ld_stream<nt_loads(NTS)>(src + ((uint64_t)(k * NB) << les)));
+            }
+        });
+    }
+    // ---- twiddles and butterflies, one packed pair of butterflies at a time ----
+    if constexpr (St::first && BM == 2) {
+        C1 anc0[4], anc1[4];
+        if constexpr (share_anc) {
+            anc0[0] = cmul(twp[1], twp[0]);
+#pragma unroll
+            for (int i = 1; (1 << i) < q; i++) anc0[i] = cmul(anc0[i - 1], anc0[i - 1]);
+        }
+#pragma unroll
+        for (int m = 0; m < U / 2; m++) {
+            if constexpr (!share_anc) {
+                anc0[0] = cmul(twp[4 * (2 * m) + 1], twp[4 * (2 * m) + 0]);
+                anc1[0] = cmul(twp[4 * (2 * m + 1) + 1], twp[4 * (2 * m + 1) + 0]);
+#pragma unroll
+                for (int i = 1; (1 << i) < q; i++) {
+                    anc0[i] = cmul(anc0[i - 1], anc0[i - 1]);
+                    anc1[i] = cmul(anc1[i - 1], anc1[i - 1]);
+                }
+            }
+            CP ap[4];
+#pragma unroll
+            for (int i = 0; (1 << i) < q; i++) ap[i] = pk_pair(anc0[i], share_anc ? anc0[i] : anc1[i]);
+            apply_powers<q>(&vp[m * q], ap);
+            dft<q>(&vp[m * q]);
+            const CP base = pk_pair(cmul(twp[4 * (2 * m) + 3], twp[4 * (2 * m) + 2]),
+                                    cmul(twp[4 * (2 * m + 1) + 3], twp[4 * (2 * m + 1) + 2]));
+#pragma unroll
+            for (int k = 0; k < q; k++) vp[m * q + k] = cmul(vp[m * q + k], base);
+        }
+    } else if constexpr (!St::first) {
+        // w_{ns q}^{(b mod ns) k} = w_R^{(b mod ns) k R/(ns q)}, per butterfly
+        const C1* __restrict__ twr = static_cast<const C1*>(a.tw_r);
+#pragma unroll
+        for (int m = 0; m < U / 2; m++) {
+            int c0, b0, c1, b1;
+            St::map(tid, 2 * m, c0, b0);
+            St::map(tid, 2 * m + 1, c1, b1);
+            const int e0 = (b0 & (ns - 1)) * (R / (ns * q)), e1 = (b1 & (ns - 1)) * (R / (ns * q));
+            CP ap[4];
+#pragma unroll
+            for (int i = 0; (1 << i) < q; i++) ap[i] = pk_pair(twr[e0 << i], twr[e1 << i]);
+            apply_powers<q>(&vp[m * q], ap);
+            dft<q>(&vp[m * q]);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < U / 2; m++) dft<q>(&vp[m * q]);
+    }
+
+    if constexpr (St::last) {
+        // ---- outputs r' = b + k NB straight to HBM ----
+        C1* __restrict__ out = static_cast<C1*>(a.out);
+        static_for<0, U, 1>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            int c, b;
+            St::map(tid, u, c, b);
+            const uint64_t line = tile * C + c;
+            if (line < a.nlines) {
+                const uint64_t bt = line >> log_lb, j = line & lb_mask;
+                const uint32_t lns = (uint32_t)log_ns;
+                const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
+                const uint64_t pad = (j >> a.out_pad_log) * a.out_pad;
+                C1* dst = out + bt * a.out_bstride + pos + pad;
+#pragma unroll
+                for (int k = 0; k < q; k++)
+                    st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << lns), pk_get<u & 1>(vp[(u >> 1) * q + k]));
+            }
+        });
+    } else {
+        // ---- exchange with stage S+1 through LDS, one component at a time ----
+        using Nx = Stage<R, C, BM, S + 1, VPT>;
+        static_assert(Nx::U % 2 == 0, "butterflies go in pairs");
+#pragma unroll
+        for (int comp = 0; comp < 2; comp++) {
+            if (S > 0 || comp > 0) __syncthreads();
+            static_for<0, U, 1>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                int c, b;
+                St::map(tid, u, c, b);
+                const int base = (b / ns) * ns * q + (b & (ns - 1));  // r' = base + k ns
+#pragma unroll
+                for (int k = 0; k < q; k++) {
+                    const C1 x = pk_get<u & 1>(vp[(u >> 1) * q + k]);
+                    lds[lds_at(LL, c, base + k * ns)] = comp ? x.im : x.re;
+                }
+            });
+            __syncthreads();
+            static_for<0, Nx::U, 1>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                int c, b;
+                Nx::map(tid, u, c, b);
+#pragma unroll
+                for (int k = 0; k < Nx::q; k++) {
+                    const float x = lds[lds_at(LL, c, b + k * Nx::NB)];
+                    CP& d = vp[(u >> 1) * Nx::q + k];
+                    if (comp) {
+                        if constexpr (u & 1) d.im.y = x; else d.im.x = x;
+                    } else {
+                        if constexpr (u & 1) d.re.y = x; else d.re.x = x;
+                    }
+                }
+            });
+        }
+        pass_stages_packed<R, C, MODE, NTS, S + 1>(a, lds, vp, tid, tile, twp);
+    }
+}
+
+#ifndef PIFFT_PACK32
+#define PIFFT_PACK32 1  // VPT-32 fp32 instances: the packed form (0: the scalar form, which spills)
+#endif
 // inter-pass twiddle entries fetched with a tile's first-stage loads (MODE 2)
 template <int R, int C, int MODE, int VPT>
 constexpr int first_tw_count() {
@@ -1062,7 +1268,14 @@ void k_pass(PassArgs a) {
     uint64_t tile = tile_of_block(blockIdx.x, a.log_xg, gridDim.x);
     T* lds = reinterpret_cast<T*>(pifft_smem);
     const int tid = (int)threadIdx.x;
-    if constexpr (H == 1) {
+    if constexpr (VPT == 32 && std::is_same_v<T, float> && PIFFT_PACK32) {
+        static_assert(H == 1, "packed VPT-32: one tile per workgroup");
+        cx<f2> vp[PassShape<R, VPT>::Q / 2];
+        cx<float> twp[TWN];
+        pass_stages_packed<R, C, MODE, NTS, 0>(a, reinterpret_cast<float*>(pifft_smem), vp, tid, tile, twp);
+        (void)pre;
+        (void)lds;
+    } else if constexpr (H == 1) {
         if (a.ilv_log && a.log_lb >= (uint32_t)ilog2c(C)) {
             // natural-order store: the P workers' tiles of one line block run
             // back to back (and on one XCD, log_xg >= log2 P), so the P 16-B

@@ -248,3 +248,29 @@ def test_subtiled_passes_bitwise_equal(prec, passes, monkeypatch):
     sub.execute_device(x.data_ptr(), yb.data_ptr(), st)
     torch.cuda.synchronize()
     assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb))
+
+
+def test_packed_vpt32_fp32_three_pass_bitwise(monkeypatch):
+    """fp32 2^28 in three passes on the 16384-value tile: the packed VPT-32
+    passes (512 threads, two butterflies per register pair, PIFFT_VPT32=1)
+    equal the 16-values-per-thread passes (1024 threads) bit for bit -- the
+    same radices, twiddles and operation order -- and the oracle within the
+    fp32 tolerance (a spot check of 64 bins)."""
+    n = 1 << 28
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F32, seed=33, stream=st)
+    monkeypatch.setenv("PIFFT_TILE32", "16384")
+    monkeypatch.setenv("PIFFT_PASSES", "3")
+    v16 = pifft.Plan(n, 1, 1, pifft.F32)
+    monkeypatch.setenv("PIFFT_VPT32", "1")
+    v32 = pifft.Plan(n, 1, 1, pifft.F32)
+    assert v16.describe()["radix"] == v32.describe()["radix"] == [1024, 512, 512]
+    assert v16.describe()["vpt"] == [16, 16, 16] and v32.describe()["vpt"] == [32, 32, 32]
+    ya = torch.empty_like(x)
+    v16.execute_device(x.data_ptr(), ya.data_ptr(), st)
+    v16.close()
+    yb = torch.empty_like(x)
+    v32.execute_device(x.data_ptr(), yb.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb))
