@@ -291,13 +291,15 @@ int tile_elems(int prec) {
     return env_int(prec == 64 ? "PIFFT_TILE64" : "PIFFT_TILE32", 8192);
 }
 
-int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines, const char* env_c, int mode) {
+int pick_lines(int prec, int R, uint64_t ntrans_lines_cap, uint64_t total_lines, const char* env_c, int mode,
+               int strided_tile = 0) {
     int C = env_int(env_c, 0);
     // single pass: lines are whole contiguous transforms, no segment-width
     // constraint -> small tiles (measured best: C = 4096/R, i.e. C=1 at 4096)
     int tile = mode == 0   ? env_int(prec == 64 ? "PIFFT_SINGLE_TILE64" : "PIFFT_SINGLE_TILE32", 4096)
                : mode == 1 ? env_int(prec == 64 ? "PIFFT_FIRST_TILE64" : "PIFFT_FIRST_TILE32", tile_elems(prec))
                            : tile_elems(prec);
+    if (strided_tile && (mode == 1 || mode == 2)) tile = strided_tile;  // (the packed VPT-32 fp32 tile)
     // fp64 strided passes of R <= 256, not the fused tree pass (mode 3): a
     // 4096-value tile.  At 8192 (R = 256, C = 32, 512 threads) the kernel
     // spills 20 B/lane at its 128-VGPR budget; at C = 16 it runs 256 threads
@@ -350,11 +352,29 @@ double seg_rate(double seg_bytes) {
 // the rate of its narrowest strided side (C*esz-byte row segments).
 // heavy_first: the first pass also evaluates the tree (reads P leaves per
 // input, P = 2^lp), so its read side dominates.
-int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, int heavy_lp = 0) {
+// fp32 strided passes at 32 values per thread, packed (k_pass VPT 32): a
+// 16384-value tile on 512 threads, two workgroups per CU -- the bytes and
+// row-segment widths of the fp64 8192-value tile, so fp32 2^28 runs in three
+// passes (1024-512-512 at C = 16/32/32) instead of four 128-point ones.
+// Measured on MI355X (profiles/r03_fp32_packed_vpt32.log): fp32 2^28 3.36 ->
+// 2.67 ms, 2^30 13.7 -> 11.6 ms; 2^26 (512 MiB per side) 0.63 -> 0.65 ms.
+// The rule: data beyond 1 GiB per side, no fused tree pass (no packed MODE 3
+// instances).  PIFFT_VPT32: -1 this rule, 0 never, 1 whenever instantiated.
+bool use_vpt32(int prec, uint64_t M, uint64_t ntrans, int heavy_lp) {
+    const int force = env_int("PIFFT_VPT32", -1);
+    if (prec != 32 || heavy_lp || force == 0) return false;
+    return force == 1 || ntrans * M * 8 >= (1ull << 30);
+}
+
+int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, int heavy_lp = 0,
+                bool allow_v32 = true) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
     const size_t esz = prec == 64 ? 16 : 8;
+    const bool v32 = allow_v32 && M > (1ull << env_int("PIFFT_SINGLE_MAX_LOG", 14)) &&
+                     use_vpt32(prec, M, ntrans, heavy_lp);
+    const int stile = v32 ? 16384 : 0;
     const int nts = pick_nts(2 * ntrans * M * esz);
     const int single_max = env_int("PIFFT_SINGLE_MAX_LOG", 14);
     if (logm <= single_max) {
@@ -389,7 +409,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
                 const int R = 1 << logs[p], mode = p == 0 ? 1 : 2;
                 const int C = pick_lines(prec, R, M >> logs[p], ntrans * (M >> logs[p]),
                                          prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32",
-                                         (p == 0 && heavy_lp) ? 3 : mode);
+                                         (p == 0 && heavy_lp) ? 3 : mode, stile);
                 if (!find_pass(prec, R, C, mode, nts)) return fail("no pass kernel R=%d C=%d", R, C);
                 out.push_back({R, C, mode, nts});
             }
@@ -433,7 +453,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
                 const int mode = p == 0 ? 1 : 2;
                 const int C = pick_lines(prec, R, M >> bits, ntrans * (M >> bits),
                                          prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32",
-                                         (p == 0 && heavy_lp) ? 3 : mode);
+                                         (p == 0 && heavy_lp) ? 3 : mode, stile);
                 if (!find_pass(prec, R, C, mode, nts)) { ok = false; break; }
                 const double rs = seg_rate((double)C * esz);           // strided side
                 const double side = (double)ntrans * M * esz * 1e-12;  // TB per side
@@ -459,11 +479,16 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             if (h > 1 && find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, pc.vpt, h)) pc.h = h;
         }
     }
-    // tuning: fp32 strided passes at 32 values per thread (512 threads over
-    // the 16384-value tile, PIFFT_TILE32=16384, two workgroups per CU)
-    if (prec == 32 && env_int("PIFFT_VPT32", 0))
-        for (auto& pc : out)
-            if ((pc.mode == 1 || pc.mode == 2) && find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, 32)) pc.vpt = 32;
+    // the packed VPT-32 passes for the 16384-value tile (every strided pass
+    // must have its instance, else the plan is redone at the 8192 tile)
+    if (v32) {
+        for (auto& pc : out) {
+            if (pc.mode != 1 && pc.mode != 2) continue;
+            if (!find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, 32))
+                return plan_passes(M, prec, ntrans, out, heavy_lp, false);
+            pc.vpt = 32;
+        }
+    }
     // tuning: lines per workgroup of the last pass (its write side's segment width)
     const int last_c = env_int("PIFFT_LAST_C", 0);
     if (last_c > 0 && out.size() > 1 && find_pass(prec, out.back().R, last_c, out.back().mode, out.back().nts))

@@ -114,9 +114,17 @@ def test_config5_2e32_one_worker_of_8():
     assert pifft.dry_run(1 << 28, 8, 1, F64, first=7, count=1)["radix"] == [512, 256, 256]
 
 
-def test_fp32_large_prefers_wide_segments():
+def test_fp32_large_prefers_wide_segments(monkeypatch):
+    """fp32 beyond 1 GiB per side: three passes on the 16384-value tile with
+    the packed 32-values-per-thread passes (C4's segment widths: 128 B on the
+    first pass's read side, 256 B after); below it, or with PIFFT_VPT32=0, the
+    8192-value tile with >= 256-B row segments everywhere."""
     d = pifft.dry_run(1 << 28, 1, 1, F32)
-    assert all(c * 8 >= 256 for c in d["lines"])  # >= 256-B row segments on every strided side
+    assert d["radix"] == [1024, 512, 512] and d["lines"] == [16, 32, 32] and d["vpt"] == [32, 32, 32]
+    assert pifft.dry_run(1 << 26, 1, 1, F32)["vpt"] == [16, 16, 16]
+    monkeypatch.setenv("PIFFT_VPT32", "0")
+    d = pifft.dry_run(1 << 28, 1, 1, F32)
+    assert all(c * 8 >= 256 for c in d["lines"]) and set(d["vpt"]) == {16}
 
 
 @pytest.mark.parametrize("n,P,kinds", [
@@ -178,11 +186,11 @@ def test_padded_workspace_rows(monkeypatch):
     padded = ws(1 << 28)
     monkeypatch.setenv("PIFFT_W_PAD", "0")
     assert padded - ws(1 << 28) == 512 * 1040 * 16
-    # fp32 2^28 (four passes 128^4): both workspace hand-offs read 128 rows
+    # fp32 2^28 (three packed passes 1024 x 512 x 512): the last hand-off reads 512 rows
     monkeypatch.delenv("PIFFT_W_PAD")
     padded32 = ws(1 << 28, prec=F32)
     monkeypatch.setenv("PIFFT_W_PAD", "0")
-    assert padded32 - ws(1 << 28, prec=F32) == 128 * 2080 * 8
+    assert padded32 - ws(1 << 28, prec=F32) == 512 * 2080 * 8
     monkeypatch.delenv("PIFFT_W_PAD")
     small = ws(1 << 28, 8, first=0, count=1, flags=pifft.OUT_SLICES)
     monkeypatch.setenv("PIFFT_W_PAD", "0")

@@ -79,7 +79,9 @@ for R in (512, 1024, 2048):
 # fp32 strided passes at 32 values per thread: a 16384-value tile (the bytes
 # and row-segment widths of the fp64 8192-value tile) on 512 threads, two
 # workgroups per CU (PIFFT_VPT32; three passes 1024-512-512 at 2^28)
-for R in (256, 512, 1024, 2048):
+# (R = 512 and 1024: the radices of 2^27-2^30 three-pass plans; 256 and 2048
+# spill 44-100 B per lane in this form)
+for R in (512, 1024):
     C = 16384 // R
     for nts in (0, 1):
         for mode in (1, 2):
