@@ -393,6 +393,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         return 0;
     }
     // tuning: explicit log2 radices, e.g. PIFFT_RADIX_LOGS=10,10,8 (must sum to log2 M)
+    bool explicit_radices = false;
     if (const char* rl = getenv("PIFFT_RADIX_LOGS")) {
         std::vector<int> logs;
         for (const char* c = rl; *c;) {
@@ -413,7 +414,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
                 if (!find_pass(prec, R, C, mode, nts)) return fail("no pass kernel R=%d C=%d", R, C);
                 out.push_back({R, C, mode, nts});
             }
-            return 0;
+            explicit_radices = true;
         }
     }
     const int rmax_log = env_int(prec == 64 ? "PIFFT_COL_RMAX_LOG64" : "PIFFT_COL_RMAX_LOG32", 10);
@@ -424,7 +425,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
     // segments: fewest passes there
     const bool resident = 2 * ntrans * M * esz <= (256ull << 20);
     const int klast = resident && env_int("PIFFT_PASSES", 0) <= 0 ? kmin : kmax;
-    for (int k = env_int("PIFFT_PASSES", 0) > 0 ? kmax : kmin; k <= klast; k++) {
+    for (int k = env_int("PIFFT_PASSES", 0) > 0 ? kmax : kmin; k <= klast && !explicit_radices; k++) {
         if (logm < 4 * k) break;  // every radix >= 16
         const int base = logm / k, extra = logm % k;
         const int force_order = env_int("PIFFT_ORDER", -1);  // tuning: 0 or 1 only

@@ -164,8 +164,9 @@ def test_config5_all_workers_n2e32():
 @pytest.mark.timeout(600)
 def test_config4_fp32_full_size_vs_oracle():
     """The reference's own precision (data_t = float, CPU.c:33-36) at N = 2^28:
-    the 4-pass 128^4 fp32 plan and the 8-worker plan against the oracle (fp32
-    restatement, 16 workers).  Bar: rel-L2 <= 1e-5 log2 N."""
+    the default fp32 plan (three packed 32-value passes 1024 x 512 x 512) and
+    the 8-worker plan against the oracle (fp32 restatement, 16 workers).
+    Bar: rel-L2 <= 1e-5 log2 N."""
     n, logn = 1 << 28, 28
     st = torch.cuda.current_stream()
     x = torch.empty(n, dtype=torch.complex64, device="cuda")
@@ -173,6 +174,8 @@ def test_config4_fp32_full_size_vs_oracle():
     got = {}
     for P in (1, 8):
         plan = pifft.Plan(n, P, 1, pifft.F32)
+        if P == 1:
+            assert plan.describe()["vpt"] == [32, 32, 32]
         y = torch.empty_like(x)
         plan.execute_device(x.data_ptr(), y.data_ptr(), st)
         torch.cuda.synchronize()
@@ -236,6 +239,7 @@ def test_subtiled_passes_bitwise_equal(prec, passes, monkeypatch):
     pifft.generate_device(x.data_ptr(), n, n, prec, seed=21, stream=st)
     if passes != "0":
         monkeypatch.setenv("PIFFT_PASSES", passes)
+        monkeypatch.setenv("PIFFT_VPT32", "0")  # sub-tiles are a 16-value form
     base = pifft.Plan(n, 1, 1, prec)
     monkeypatch.setenv("PIFFT_SUBTILES", "2")
     sub = pifft.Plan(n, 1, 1, prec)
@@ -254,14 +258,16 @@ def test_packed_vpt32_fp32_three_pass_bitwise(monkeypatch):
     """fp32 2^28 in three passes on the 16384-value tile: the packed VPT-32
     passes (512 threads, two butterflies per register pair, PIFFT_VPT32=1)
     equal the 16-values-per-thread passes (1024 threads) bit for bit -- the
-    same radices, twiddles and operation order -- and the oracle within the
-    fp32 tolerance (a spot check of 64 bins)."""
+    same radices, twiddles and operation order. (The packed plan is fp32
+    2^28's default, so test_config4_fp32_full_size_vs_oracle checks it
+    against the oracle.)"""
     n = 1 << 28
     st = torch.cuda.current_stream()
     x = torch.empty(n, dtype=torch.complex64, device="cuda")
     pifft.generate_device(x.data_ptr(), n, n, pifft.F32, seed=33, stream=st)
     monkeypatch.setenv("PIFFT_TILE32", "16384")
     monkeypatch.setenv("PIFFT_PASSES", "3")
+    monkeypatch.setenv("PIFFT_VPT32", "0")
     v16 = pifft.Plan(n, 1, 1, pifft.F32)
     monkeypatch.setenv("PIFFT_VPT32", "1")
     v32 = pifft.Plan(n, 1, 1, pifft.F32)
