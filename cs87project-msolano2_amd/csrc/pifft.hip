@@ -14,7 +14,7 @@
 // the tree uses the reference's own omega(N,k) formula up to N = 2^22 so that
 // its output is bit-identical to the reference's post-tree segment).
 #ifndef _GNU_SOURCE
-#define _GNU_SOURCE  // sincos (reference_omega)
+#define _GNU_SOURCE  // sincos (reference_omega_levels)
 #endif
 #include "pifft_gather.h"
 #include "pifft_kernels.h"
@@ -229,18 +229,27 @@ struct TableBuilder {
         }
         return off;
     }
-    // omega(N,k), k < count, with the reference's own formula (CPU.c:644-651)
-    size_t reference_omega(uint64_t N, uint64_t count) {
+    // omega(N,k) with the reference's own formula (CPU.c:644-651), packed by
+    // tree level (TreeTw::direct): level t < levels holds omega(N, k 2^t),
+    // k < N >> (t+1), at N - (N >> t) + k (level 0 = every k < N/2)
+    size_t reference_omega_levels(uint64_t N, int levels) {
         size_t off = align();
         // gcc -O1 and up folds the reference's cos()/sin() pair into one glibc
         // sincos() call; glibc's sincos and its separate cos/sin disagree in
         // the last fp64 bit for ~1e-3 of the angles (43 of 2^15 at N=2^16).
         // The reference build the fixtures pin (-O2) is the sincos one, so the
         // table is built the same way (clang keeps the pair separate).
-        for (uint64_t k = 0; k < count; k++) {
+        for (uint64_t k = 0; k < N / 2; k++) {
             double s, c;
             sincos(2.0 * M_PI / (double)N * (double)k, &s, &c);
             put(c, -s);
+        }
+        // the higher levels: byte copies of level-0 entries k 2^t
+        blob.resize(off + (N - (N >> (levels > 0 ? levels : 1))) * esz);
+        for (int t = 1; t < levels; t++) {
+            const uint64_t base = N - (N >> t);
+            for (uint64_t k = 0; k < (N >> (t + 1)); k++)
+                memcpy(&blob[off + (base + k) * esz], &blob[off + (k << t) * esz], esz);
         }
         return off;
     }
@@ -711,7 +720,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         const int direct_max = env_int("PIFFT_TREE_DIRECT_MAX_LOG", 22);
         if (p->log_n <= direct_max) {
             tree_is_direct = true;
-            tree_direct = tb.reference_omega(p->n, p->n / 2);
+            tree_direct = tb.reference_omega_levels(p->n, p->lp);
         } else {
             tree2 = two_level(tb, p->n);
         }
@@ -739,6 +748,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         ttw.lo = tree_is_direct ? nullptr : twp(tree2.lo);
         ttw.hi = tree_is_direct ? nullptr : twp(tree2.hi);
         ttw.h = tree2.h;
+        ttw.log_n = (uint32_t)p->log_n;
     }
     // One worker on this plan, a multi-pass local FFT and log2 P <= 4: fuse the
     // tree into the first pass (its P leaves per input instead of a separate

@@ -264,16 +264,30 @@ __device__ __forceinline__ void static_for(F&& f) {
 // Tree ("funnel") network, shared by k_tree and the fused first pass
 // ---------------------------------------------------------------------------
 struct TreeTw {
-    const void* direct;  // omega(N, e), e < N/2, the reference formula (CPU.c:644-651); or null
+    // The reference formula omega(N, e) (CPU.c:644-651), packed by tree level:
+    // level t's entries omega(N, k 2^t), k < N >> (t+1), sit contiguously at
+    // N - (N >> t) + k, so a level's lookups i, i+1, ... read consecutive
+    // entries (a single N/2 table read at e = k 2^t touches a whole line per
+    // 2^-t of its entries); or null
+    const void* direct;
     const void* lo;      // else two-level w_N
     const void* hi;
     uint32_t h;
+    uint32_t log_n;
 };
 
+// omega(N, e), any e < N/2 (two-level table only)
 template <typename T>
 __device__ __forceinline__ cx<T> tree_tw(const TreeTw& tw, uint64_t e) {
-    if (tw.direct) return static_cast<const cx<T>*>(tw.direct)[e];
     return tw2(static_cast<const cx<T>*>(tw.lo), static_cast<const cx<T>*>(tw.hi), tw.h, e);
+}
+
+// omega(N, k 2^t), k < N >> (t+1): the level-t twiddle of butterfly k
+template <typename T>
+__device__ __forceinline__ cx<T> tree_tw_lv(const TreeTw& tw, uint64_t k, uint32_t t) {
+    if (tw.direct)
+        return static_cast<const cx<T>*>(tw.direct)[(1ull << tw.log_n) - (1ull << (tw.log_n - t)) + k];
+    return tree_tw<T>(tw, k << t);
 }
 
 // Levels t0 .. t0+L-1 of the reference's radix-2 tree (CPU.c:419-448; level t
@@ -337,10 +351,8 @@ __device__ __forceinline__ void tree_levels(cx<T>* v, const TreeTw& tw, uint64_t
             for (int ml = 0; ml < H; ml++) {
                 const cx<T> x0 = v[lo + ml], x1 = v[lo + ml + H];
                 if (needL) v[lo + ml] = cadd(x0, x1);                      // butterfly_left
-                if (needR) {                                               // butterfly_right
-                    const uint64_t e = (i + ((uint64_t)ml << log_d)) << t;  // b * N/size
-                    v[lo + ml + H] = cmul(csub(x0, x1), tree_tw<T>(tw, e));
-                }
+                if (needR)  // butterfly_right: omega(N, b N/size), b = i + ml D
+                    v[lo + ml + H] = cmul(csub(x0, x1), tree_tw_lv<T>(tw, i + ((uint64_t)ml << log_d), t));
             }
         }
     }
@@ -357,10 +369,8 @@ __device__ __forceinline__ cx<T> tree_path(cx<T>* v, const TreeTw& tw, uint64_t 
         const int H = (1 << LP) >> (t + 1);
         if ((q >> (LP - 1 - t)) & 1) {
 #pragma unroll
-            for (int ml = 0; ml < H; ml++) {
-                const uint64_t e = (i + ((uint64_t)ml << log_m)) << t;
-                v[ml] = cmul(csub(v[ml], v[ml + H]), tree_tw<T>(tw, e));
-            }
+            for (int ml = 0; ml < H; ml++)
+                v[ml] = cmul(csub(v[ml], v[ml + H]), tree_tw_lv<T>(tw, i + ((uint64_t)ml << log_m), t));
         } else {
 #pragma unroll
             for (int ml = 0; ml < H; ml++) v[ml] = cadd(v[ml], v[ml + H]);
@@ -822,7 +832,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 const uint64_t zi0 = j + ((uint64_t)b << log_lb);
                 C2 bt[LP];
 #pragma unroll
-                for (int t = 0; t < LP; t++) bt[t] = tree_tw<T>(a.tree, zi0 << t);
+                for (int t = 0; t < LP; t++) bt[t] = tree_tw_lv<T>(a.tree, zi0, t);
                 static_for<0, q, G>([&](auto k0c) {
                     constexpr int k0 = decltype(k0c)::value;
                     C2 w[G][P];
