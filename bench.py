@@ -409,6 +409,12 @@ class Job:
                "kernel_ms_per_step": round(dom_step_ms, 6), "all_launches_ms_per_step": round(kernel_step_ms, 6),
                "step_ms": round(ms_per_step, 6), "event_ms_per_step": round(raw_step_ms, 6),
                "event_overhead_subtracted_ms": round(raw_step_ms - kernel_step_ms, 6)}
+        # the whole step beside the dominant kernel: every launch's algorithmic
+        # bytes over the measured step time (a plan may trade one kernel's
+        # frac for a shorter step, e.g. the narrow-segment pass moved last)
+        step_bytes = sum(d["launch_bytes"][:nl])
+        rec["step_achieved"] = round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1) if ms_per_step > 0 else None
+        rec["step_frac"] = round(rec["step_achieved"] / HBM_PEAK_GBS, 4) if rec["step_achieved"] else None
         if dom_ms <= 0 or dom_step_ms > ms_per_step * (1 + 1e-9) or kernel_step_ms > ms_per_step * (1 + 1e-9):
             rec.update({"achieved": None, "frac": None,
                         "error": f"refused: launches take {kernel_step_ms:.6f} ms (dominant {dom_step_ms:.6f} ms) "

@@ -355,6 +355,21 @@ double seg_rate(double seg_bytes) {
     return 1.5;
 }
 
+// Whole-pass HBM rate (TB/s, both sides) by the pass's position in a plan and
+// its strided row-segment width, for HBM-bound plans without a fused tree
+// (round 3).  Measured on MI355X (profiles/r03_fp64_radix_order.log,
+// r03_fp32_radix_order.log; fp64 2^28 / 2^29, fp32 packed 2^28): a 256-B pass
+// runs 5.9 / 5.6 / 5.25 TB/s first / in the middle / last, a 128-B one 5.0 /
+// 4.8 / 4.8 -- the last pass's strided stores into the caller's unpadded
+// output are slow at either width, so the narrow pass costs least there.
+// fp64 2^28: 512-512-1024 4.72 ms vs 1024-512-512 4.82 (same box); fp32 2^28
+// 2.47 vs 2.60 ms; fp64 2^29 9.41 vs 9.65 ms.  Same for both precisions.
+double pass_rate(double seg_bytes, bool first, bool last) {
+    if (seg_bytes >= 256) return first ? 5.9 : last ? 5.25 : 5.6;
+    if (seg_bytes >= 128) return first ? 5.0 : 4.8;
+    return seg_rate(seg_bytes);
+}
+
 // Local FFT of length M as passes.  A single LDS/register-resident pass when M
 // fits (M <= 2^14); otherwise k Stockham passes with balanced radices, k and
 // the radix order chosen by a bandwidth model: each pass moves its bytes at
@@ -468,7 +483,10 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
                 const double rs = seg_rate((double)C * esz);           // strided side
                 const double side = (double)ntrans * M * esz * 1e-12;  // TB per side
                 const double reads = (p == 0 && heavy_lp) ? side * (1 << heavy_lp) : side;
-                cost += reads / rs + side / (mode == 1 ? 5.6 : rs);
+                if (!resident && !heavy_lp && env_int("PIFFT_POS_MODEL", 1))
+                    cost += 2 * side / pass_rate((double)C * esz, p == 0, p == k - 1);
+                else
+                    cost += reads / rs + side / (mode == 1 ? 5.6 : rs);
                 cand.push_back({R, C, mode, nts});
             }
             if (ok && cost < best) {
@@ -1437,27 +1455,32 @@ int pifft_plan_tune_workspace(pifft_plan* p, const void* d_in, void* d_out, void
     int rc = 0;
     float best = 0.0f;
     if (timed(best)) rc = -1;
+    // every losing workspace stays allocated until the end, so each try lands
+    // somewhere new (a freed range would come straight back from hipMalloc)
+    std::vector<void*> losers;
     for (int t = 1; t < tries && rc == 0; t++) {
         void* keep = p->buf[BUF_W];
         void* fresh = nullptr;
         if (hipMalloc(&fresh, p->bytes_w) != hipSuccess) {
             (void)hipGetLastError();
-            break;  // no room for a second workspace: keep the first
+            break;  // no room for another workspace: keep the best so far
         }
         p->buf[BUF_W] = fresh;
         float ms = 0.0f;
         if (timed(ms)) {
             rc = -1;
+            p->buf[BUF_W] = keep;
+            losers.push_back(fresh);
         } else if (ms < best) {
             best = ms;
-            (void)hipStreamSynchronize(st);
-            (void)hipFree(keep);
-            continue;
+            losers.push_back(keep);
+        } else {
+            p->buf[BUF_W] = keep;
+            losers.push_back(fresh);
         }
-        (void)hipStreamSynchronize(st);
-        p->buf[BUF_W] = keep;
-        (void)hipFree(fresh);
     }
+    (void)hipStreamSynchronize(st);
+    for (void* w : losers) (void)hipFree(w);
     (void)hipEventDestroy(e[0]);
     (void)hipEventDestroy(e[1]);
     if (best_ms) *best_ms = best;

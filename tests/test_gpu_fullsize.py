@@ -227,12 +227,17 @@ def test_reference_max_size_n2e30_fp64():
     assert err2 <= TOL64, err2
 
 
+ORDERS = {"0": [1024, 512, 512], "1": [512, 512, 1024]}  # PIFFT_POS_MODEL: the radix order at 2^28
+
+
+@pytest.mark.parametrize("pos", ["0", "1"])
 @pytest.mark.parametrize("prec,passes", [(pifft.F64, "0"), (pifft.F32, "3")])
-def test_subtiled_passes_bitwise_equal(prec, passes, monkeypatch):
+def test_subtiled_passes_bitwise_equal(prec, passes, pos, monkeypatch):
     """k_pass with two sub-tiles per workgroup (H = 2, PIFFT_SUBTILES) runs the
     same per-line arithmetic as H = 1: the 2^28 plan's output is bitwise
-    equal (fp64 1024-512-512, fp32 forced to the same three passes)."""
+    equal (fp64, fp32 forced to three passes; both radix orders)."""
     n = 1 << 28
+    monkeypatch.setenv("PIFFT_POS_MODEL", pos)
     cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
     st = torch.cuda.current_stream()
     x = torch.empty(n, dtype=cdt, device="cuda")
@@ -243,7 +248,7 @@ def test_subtiled_passes_bitwise_equal(prec, passes, monkeypatch):
     base = pifft.Plan(n, 1, 1, prec)
     monkeypatch.setenv("PIFFT_SUBTILES", "2")
     sub = pifft.Plan(n, 1, 1, prec)
-    assert base.describe()["radix"] == sub.describe()["radix"] == [1024, 512, 512]
+    assert base.describe()["radix"] == sub.describe()["radix"] == ORDERS[pos]
     assert [2 * c for c in base.describe()["lines"]] == sub.describe()["lines"]
     ya = torch.empty_like(x)
     base.execute_device(x.data_ptr(), ya.data_ptr(), st)
@@ -254,14 +259,16 @@ def test_subtiled_passes_bitwise_equal(prec, passes, monkeypatch):
     assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb))
 
 
-def test_packed_vpt32_fp32_three_pass_bitwise(monkeypatch):
+@pytest.mark.parametrize("pos", ["0", "1"])
+def test_packed_vpt32_fp32_three_pass_bitwise(pos, monkeypatch):
     """fp32 2^28 in three passes on the 16384-value tile: the packed VPT-32
     passes (512 threads, two butterflies per register pair, PIFFT_VPT32=1)
     equal the 16-values-per-thread passes (1024 threads) bit for bit -- the
     same radices, twiddles and operation order. (The packed plan is fp32
     2^28's default, so test_config4_fp32_full_size_vs_oracle checks it
-    against the oracle.)"""
+    against the oracle.)  Both radix orders."""
     n = 1 << 28
+    monkeypatch.setenv("PIFFT_POS_MODEL", pos)
     st = torch.cuda.current_stream()
     x = torch.empty(n, dtype=torch.complex64, device="cuda")
     pifft.generate_device(x.data_ptr(), n, n, pifft.F32, seed=33, stream=st)
@@ -271,7 +278,7 @@ def test_packed_vpt32_fp32_three_pass_bitwise(monkeypatch):
     v16 = pifft.Plan(n, 1, 1, pifft.F32)
     monkeypatch.setenv("PIFFT_VPT32", "1")
     v32 = pifft.Plan(n, 1, 1, pifft.F32)
-    assert v16.describe()["radix"] == v32.describe()["radix"] == [1024, 512, 512]
+    assert v16.describe()["radix"] == v32.describe()["radix"] == ORDERS[pos]
     assert v16.describe()["vpt"] == [16, 16, 16] and v32.describe()["vpt"] == [32, 32, 32]
     ya = torch.empty_like(x)
     v16.execute_device(x.data_ptr(), ya.data_ptr(), st)

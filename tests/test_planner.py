@@ -52,8 +52,11 @@ def test_config3_batched_fp32_single_pass():
 
 
 def test_config4_2e28_fp64():
+    """The 1024-point pass (128-B row segments at C = 8) goes last, where its
+    narrow segments cost least (planner pass_rate, measured round 3)."""
     d = pifft.dry_run(1 << 28, 1, 1, F64)
-    assert d["radix"] == [1024, 512, 512] and d["lines"] == [8, 16, 16]
+    assert d["radix"] == [512, 512, 1024] and d["lines"] == [16, 16, 8]
+    assert pifft.dry_run(1 << 29, 1, 1, F64)["radix"] == [512, 1024, 1024]
     assert d["launch_bytes"] == [2 * (1 << 28) * 16] * 3
     assert d["workspace_bytes"] >= 4 * GiB and d["chunk_pairs"] == 0
 
@@ -116,11 +119,12 @@ def test_config5_2e32_one_worker_of_8():
 
 def test_fp32_large_prefers_wide_segments(monkeypatch):
     """fp32 beyond 1 GiB per side: three passes on the 16384-value tile with
-    the packed 32-values-per-thread passes (C4's segment widths: 128 B on the
-    first pass's read side, 256 B after); below it, or with PIFFT_VPT32=0, the
-    8192-value tile with >= 256-B row segments everywhere."""
+    the packed 32-values-per-thread passes (C4's segment widths: 256 B, and
+    128 B on the last pass, where the narrow pass costs least); below it, or
+    with PIFFT_VPT32=0, the 8192-value tile with >= 256-B row segments
+    everywhere."""
     d = pifft.dry_run(1 << 28, 1, 1, F32)
-    assert d["radix"] == [1024, 512, 512] and d["lines"] == [16, 32, 32] and d["vpt"] == [32, 32, 32]
+    assert d["radix"] == [512, 512, 1024] and d["lines"] == [32, 32, 16] and d["vpt"] == [32, 32, 32]
     assert pifft.dry_run(1 << 26, 1, 1, F32)["vpt"] == [16, 16, 16]
     monkeypatch.setenv("PIFFT_VPT32", "0")
     d = pifft.dry_run(1 << 28, 1, 1, F32)
@@ -179,18 +183,19 @@ def test_every_multipass_worker_plan_fuses_its_tree(prec):
 
 def test_padded_workspace_rows(monkeypatch):
     """Padded workspace rows (PassArgs::in_pad/out_pad, PIFFT_W_PAD): W rows
-    16 KiB + 256 B apart for a W of 2 GiB or more (C4: 512 rows of pass 3),
+    16 KiB + 256 B apart for a W of 2 GiB or more (C4: the 1024 rows pass 3
+    reads),
     none below (the worker of 8 at 2^28: 512 MiB); PIFFT_W_PAD=0 turns it off."""
     def ws(n, P=1, prec=F64, **kw):
         return pifft.dry_run(n, P, 1, prec, **kw)["workspace_bytes"]
     padded = ws(1 << 28)
     monkeypatch.setenv("PIFFT_W_PAD", "0")
-    assert padded - ws(1 << 28) == 512 * 1040 * 16
-    # fp32 2^28 (three packed passes 1024 x 512 x 512): the last hand-off reads 512 rows
+    assert padded - ws(1 << 28) == 1024 * 1040 * 16
+    # fp32 2^28 (three packed passes 512 x 512 x 1024): the last hand-off reads 1024 rows
     monkeypatch.delenv("PIFFT_W_PAD")
     padded32 = ws(1 << 28, prec=F32)
     monkeypatch.setenv("PIFFT_W_PAD", "0")
-    assert padded32 - ws(1 << 28, prec=F32) == 512 * 2080 * 8
+    assert padded32 - ws(1 << 28, prec=F32) == 1024 * 2080 * 8
     monkeypatch.delenv("PIFFT_W_PAD")
     small = ws(1 << 28, 8, first=0, count=1, flags=pifft.OUT_SLICES)
     monkeypatch.setenv("PIFFT_W_PAD", "0")
@@ -228,3 +233,16 @@ def test_worker_interleaved_layout(monkeypatch):
     d0 = pifft.dry_run(1 << 20, 8, 1, F64)
     assert not d0["worker_interleaved"] and d0["natural_store"]
     assert pifft.dry_run(1 << 28, 8, 1, F64)["launch_kind"][-1] == "interleave"
+
+
+def test_position_model_off_restores_bandwidth_model(monkeypatch):
+    """PIFFT_POS_MODEL=0: the round-2 segment-width model (1024-point pass
+    first); plans with a fused tree or resident in the Infinity Cache never
+    used the position rates."""
+    fused = pifft.dry_run(1 << 28, 8, 1, F64, first=0, count=1)["radix"]
+    small = pifft.dry_run(1 << 20, 1, 1, F64)["radix"]
+    monkeypatch.setenv("PIFFT_POS_MODEL", "0")
+    assert pifft.dry_run(1 << 28, 1, 1, F64)["radix"] == [1024, 512, 512]
+    assert pifft.dry_run(1 << 28, 1, 1, F32)["radix"] == [1024, 512, 512]
+    assert pifft.dry_run(1 << 28, 8, 1, F64, first=0, count=1)["radix"] == fused
+    assert pifft.dry_run(1 << 20, 1, 1, F64)["radix"] == small

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--variants", default="[{}]")
     ap.add_argument("--flags", type=int, default=-1, help="plan flags (default: natural / slices)")
+    ap.add_argument("--tune-ws", type=int, default=0,
+                    help="workspace placements tried per plan (pifft_plan_tune_workspace, as bench.py does)")
     args = ap.parse_args()
     import torch
     import pifft
@@ -62,6 +64,8 @@ def main():
         d = plan.describe()
         if y is None or y.numel() != d["out_elems"]:
             y = torch.empty(d["out_elems"], dtype=cdt, device="cuda")
+        if args.tune_ws > 0:
+            plan.tune_workspace(x.data_ptr(), y.data_ptr(), tries=args.tune_ws)
         for _ in range(args.warmup):
             plan.execute_device(x.data_ptr(), y.data_ptr())
         torch.cuda.synchronize()
