@@ -284,10 +284,12 @@ def headline_cpu_baseline(log_n: int, prec: int, batch: int = 1, threads: int | 
     return rec
 
 
-def load_traffic(config_key: str, launch_indices):
+def load_traffic(config_key: str, launch_indices, kernel_names=None):
     """HBM bytes per launch of the dominant kernel (mean over its launches) from
     the committed PMC summary (the last profiles/*traffic*.json of this plan by
-    name: round tags sort in order)."""
+    name: round tags sort in order).  With kernel_names, a summary counts only
+    if it profiled those very kernels at those launches (a planner change
+    gives the same config a different plan)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))  # r02_* after r01_*
     for f in reversed(files):
         try:
@@ -296,6 +298,9 @@ def load_traffic(config_key: str, launch_indices):
             continue
         if d.get("config_key") == config_key:
             per = d.get("per_launch_bytes", {})
+            if kernel_names is not None and [d.get("kernels", {}).get(str(i), {}).get("kernel")
+                                             for i in launch_indices] != list(kernel_names):
+                continue
             vals = [per.get(str(i)) for i in launch_indices]
             if vals and all(v is not None for v in vals):
                 return float(sum(vals)) / len(vals), os.path.relpath(f, ROOT)
@@ -723,7 +728,8 @@ def main() -> int:
     desc = job.desc
     launches = job.launches(local_s * 1e3 / args.steps)
     config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
-    traffic, traffic_src = load_traffic(config_key, rf["launches"])
+    traffic, traffic_src = load_traffic(config_key, rf["launches"],
+                                        [job.plan.kernel_name(i) for i in rf["launches"]])
 
     per_rank = None
     if dist is not None:
@@ -761,7 +767,8 @@ def main() -> int:
         rf_line = {k: rf[k] for k in ("bound", "kernel", "kernel_name", "mean_ms", "achieved", "peak", "unit", "frac")}
         rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"],
                         "kernel_ms_per_step": rf["kernel_ms_per_step"],
-                        "all_launches_ms_per_step": rf["all_launches_ms_per_step"], "step_ms": rf["step_ms"]})
+                        "all_launches_ms_per_step": rf["all_launches_ms_per_step"], "step_ms": rf["step_ms"],
+                        "step_achieved": rf["step_achieved"], "step_frac": rf["step_frac"]})
         if "error" in rf:
             rf_line["error"] = rf["error"]
         line = {

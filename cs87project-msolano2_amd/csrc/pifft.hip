@@ -497,13 +497,16 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
     }
     if (out.empty()) return fail("no pass decomposition for M=2^%d", logm);
     // tuning: two sub-tiles per workgroup on the strided passes (k_pass H = 2,
-    // one workgroup per CU): PIFFT_SUBTILES=2 (every strided pass) or
-    // PIFFT_SUBTILES_FIRST=2 (the first pass only)
+    // one workgroup per CU): PIFFT_SUBTILES=2 (every strided pass),
+    // PIFFT_SUBTILES_FIRST=2 (the first pass only) or PIFFT_SUBTILES_LAST=2
+    // (the last pass only)
     {
         const int hall = env_int("PIFFT_SUBTILES", 1), hfirst = env_int("PIFFT_SUBTILES_FIRST", hall);
+        const int hlast = env_int("PIFFT_SUBTILES_LAST", hall);
         for (size_t i = 0; i < out.size(); i++) {
             PassChoice& pc = out[i];
-            const int h = (pc.mode == 1) ? hfirst : (pc.mode == 2 ? hall : 1);
+            const bool last = i + 1 == out.size() && out.size() > 1;
+            const int h = (pc.mode == 1) ? hfirst : (pc.mode == 2 ? (last ? hlast : hall) : 1);
             if (h > 1 && find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, pc.vpt, h)) pc.h = h;
         }
     }
