@@ -472,6 +472,15 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             std::vector<PassChoice> cand;
             double cost = 0.0;
             bool ok = true;
+            // the position rates were measured on passes of >= 128-B segments:
+            // a candidate with a narrower pass keeps the segment-width model
+            bool pos = !resident && !heavy_lp && env_int("PIFFT_POS_MODEL", 1);
+            for (int p = 0; p < k && pos; p++) {
+                const int bits = order ? base + (p >= k - extra ? 1 : 0) : base + (p < extra ? 1 : 0);
+                const int C = pick_lines(prec, 1 << bits, M >> bits, ntrans * (M >> bits),
+                                         prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", p == 0 ? 1 : 2, stile);
+                pos = (size_t)C * esz >= 128;
+            }
             for (int p = 0; p < k && ok; p++) {
                 const int bits = order ? base + (p >= k - extra ? 1 : 0) : base + (p < extra ? 1 : 0);
                 const int R = 1 << bits;
@@ -483,7 +492,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
                 const double rs = seg_rate((double)C * esz);           // strided side
                 const double side = (double)ntrans * M * esz * 1e-12;  // TB per side
                 const double reads = (p == 0 && heavy_lp) ? side * (1 << heavy_lp) : side;
-                if (!resident && !heavy_lp && env_int("PIFFT_POS_MODEL", 1))
+                if (pos)
                     cost += 2 * side / pass_rate((double)C * esz, p == 0, p == k - 1);
                 else
                     cost += reads / rs + side / (mode == 1 ? 5.6 : rs);
