@@ -246,3 +246,14 @@ def test_position_model_off_restores_bandwidth_model(monkeypatch):
     assert pifft.dry_run(1 << 28, 1, 1, F32)["radix"] == [1024, 512, 512]
     assert pifft.dry_run(1 << 28, 8, 1, F64, first=0, count=1)["radix"] == fused
     assert pifft.dry_run(1 << 20, 1, 1, F64)["radix"] == small
+
+
+def test_position_model_not_for_worker_interleaved_plans():
+    """All-worker plans in the worker-interleaved layout keep the segment-width
+    model's order (the narrow pass last measured 1-14 % slower there,
+    profiles/r03_pos_model_shapes.log); one-worker plans of the same local
+    size put it last."""
+    wil = pifft.dry_run(1 << 29, 2, 1, F64)
+    assert wil["worker_interleaved"] and wil["radix"] == [1024, 512, 512]
+    assert pifft.dry_run(1 << 28, 1, 1, F64)["radix"] == [512, 512, 1024]
+    assert pifft.dry_run(1 << 27, 2, 1, F32)["radix"] == [512, 512, 256]
