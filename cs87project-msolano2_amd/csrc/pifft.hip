@@ -390,8 +390,11 @@ bool use_vpt32(int prec, uint64_t M, uint64_t ntrans, int heavy_lp) {
     return force == 1 || ntrans * M * 8 >= (1ull << 30);
 }
 
+// pos_ok: the position-aware pass rates may price this plan (not for the
+// worker-interleaved layout, whose passes move rows of all workers: there the
+// narrow pass last measured 1-14 % slower, profiles/r03_pos_model_shapes.log)
 int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, int heavy_lp = 0,
-                bool allow_v32 = true) {
+                bool allow_v32 = true, bool pos_ok = true) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
@@ -474,7 +477,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             bool ok = true;
             // the position rates were measured on passes of >= 128-B segments:
             // a candidate with a narrower pass keeps the segment-width model
-            bool pos = !resident && !heavy_lp && env_int("PIFFT_POS_MODEL", 1);
+            bool pos = pos_ok && !resident && !heavy_lp && env_int("PIFFT_POS_MODEL", 1);
             for (int p = 0; p < k && pos; p++) {
                 const int bits = order ? base + (p >= k - extra ? 1 : 0) : base + (p < extra ? 1 : 0);
                 const int C = pick_lines(prec, 1 << bits, M >> bits, ntrans * (M >> bits),
@@ -525,7 +528,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         for (auto& pc : out) {
             if (pc.mode != 1 && pc.mode != 2) continue;
             if (!find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, 32))
-                return plan_passes(M, prec, ntrans, out, heavy_lp, false);
+                return plan_passes(M, prec, ntrans, out, heavy_lp, false, pos_ok);
             pc.vpt = 32;
         }
     }
@@ -669,7 +672,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const bool fuse_all = !wil_ok && p->nq > 1 && in_mib < (uint64_t)env_int("PIFFT_FUSE_ALL_MAX_MIB", 0);
     const bool may_fuse = p->P > 1 && (p->nq == 1 || fuse_all) && p->lp <= 4 && !p->separate_tree &&
                           env_int("PIFFT_FUSE_TREE", 1);
-    if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0)) return -1;
+    if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0, true, !wil_ok)) return -1;
     if (wil_ok && passes.size() > 1) {
         // the same radices, every pass a worker-interleaved MODE 2 (| 8)
         // pass at the C of a MODE 2 pass whose lines run over all workers
