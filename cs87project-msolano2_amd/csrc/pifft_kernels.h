@@ -821,12 +821,20 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             if constexpr (BM == 3) {
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
-                // to P = 8 at 128 VGPRs
+                // to P = 8 at 128 VGPRs.  Small tiles (<= 256 threads: a
+                // register budget of >= 256 VGPRs, e.g. config 2's one-GPU
+                // slice, 64 workgroups) keep more leaves in flight, so fewer
+                // dependent rounds of loads
                 constexpr int P = 1 << LP;
 #ifndef PIFFT_TREE_LOADS
 #define PIFFT_TREE_LOADS 8  // leaf loads in flight per thread and round
 #endif
-                constexpr int G = P >= PIFFT_TREE_LOADS ? 1 : PIFFT_TREE_LOADS / P;
+#ifndef PIFFT_TREE_LOADS_SMALL
+#define PIFFT_TREE_LOADS_SMALL 16  // the same for tiles of <= 256 threads
+#endif
+                constexpr int TL = PassCfg<R, C, VPT>::NT <= 256 ? PIFFT_TREE_LOADS_SMALL : PIFFT_TREE_LOADS;
+                constexpr int G = P >= TL ? 1 : TL / P;
+                static_assert(q % G == 0, "whole rounds of leaf loads");
                 const uint32_t log_m = log_lb + Sh::LOGR;
                 // this thread's base twiddles w_N^{zi0 2^t}, zi0 = its k = 0 input
                 const uint64_t zi0 = j + ((uint64_t)b << log_lb);

@@ -248,7 +248,9 @@ def test_subtiled_passes_bitwise_equal(prec, passes, pos, monkeypatch):
     base = pifft.Plan(n, 1, 1, prec)
     monkeypatch.setenv("PIFFT_SUBTILES", "2")
     sub = pifft.Plan(n, 1, 1, prec)
-    assert base.describe()["radix"] == sub.describe()["radix"] == ORDERS[pos]
+    assert base.describe()["radix"] == sub.describe()["radix"]
+    if prec == pifft.F64:  # (the fp32 8192-value tile's 1024-point pass has 64-B segments: no position model)
+        assert base.describe()["radix"] == ORDERS[pos]
     assert [2 * c for c in base.describe()["lines"]] == sub.describe()["lines"]
     ya = torch.empty_like(x)
     base.execute_device(x.data_ptr(), ya.data_ptr(), st)
