@@ -1051,6 +1051,9 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 // 174 VGPRs in MODE 2 and spills at 128).  Loads, stores and LDS exchanges
 // address each half with the VPT-32 Stage map of its own butterfly.
 // ---------------------------------------------------------------------------
+#ifndef PIFFT_PK_REMAT
+#define PIFFT_PK_REMAT 1  // packed VPT-32 exchanges: LDS addresses recomputed per component
+#endif
 using f2 = float __attribute__((ext_vector_type(2)));
 
 template <int H>
@@ -1210,10 +1213,16 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
 #pragma unroll
         for (int comp = 0; comp < 2; comp++) {
             if (S > 0 || comp > 0) __syncthreads();
+            // the second component recomputes its LDS addresses from an opaque
+            // copy of tid instead of keeping the first's 2 x 32 addresses live
+            // beside the 64 data registers (they spilled 52 B per lane in the
+            // 1024-point MODE 2 instance)
+            int tidc = tid;
+            if (PIFFT_PK_REMAT && comp) asm volatile("" : "+v"(tidc));
             static_for<0, U, 1>([&](auto uc) {
                 constexpr int u = decltype(uc)::value;
                 int c, b;
-                St::map(tid, u, c, b);
+                St::map(tidc, u, c, b);
                 const int base = (b / ns) * ns * q + (b & (ns - 1));  // r' = base + k ns
 #pragma unroll
                 for (int k = 0; k < q; k++) {
@@ -1225,7 +1234,7 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
             static_for<0, Nx::U, 1>([&](auto uc) {
                 constexpr int u = decltype(uc)::value;
                 int c, b;
-                Nx::map(tid, u, c, b);
+                Nx::map(tidc, u, c, b);
 #pragma unroll
                 for (int k = 0; k < Nx::q; k++) {
                     const float x = lds[lds_at(LL, c, b + k * Nx::NB)];
