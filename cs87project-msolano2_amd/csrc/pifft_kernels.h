@@ -532,6 +532,10 @@ struct PassCfg {
     static constexpr int waves_per_eu = wpe > 4 ? 4 : wpe;
 };
 
+#ifndef PIFFT_REMAT16
+#define PIFFT_REMAT16 0  // 16-value exchanges: LDS addresses recomputed per component (tuning)
+#endif
+
 // LDS image of a workgroup's C lines during an exchange (one component, T
 // scalars): element r of line c sits at c*ls + swz(r), swz(r) = (r XOR ((r >>
 // xs) & xm) XOR ((c & cm) << cs)) + (ps ? r >> ps : 0) -- XOR swizzles of the
@@ -1015,10 +1019,14 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int comp = 0; comp < 2; comp++) {
             // (the tile's first LDS store has no earlier reader to wait for)
             if (S > 0 || comp > 0) lds_handoff<Nx::wave_private>();
+            // PIFFT_REMAT16: the second component's LDS addresses from an opaque
+            // tid copy (as the packed VPT-32 exchange does), not kept live
+            int tidc = tid;
+            if (PIFFT_REMAT16 && comp) asm volatile("" : "+v"(tidc));
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 int c, b;
-                St::map(tid, u, c, b);
+                St::map(tidc, u, c, b);
                 const int base = (b / ns) * ns * q + (b & (ns - 1));  // r' = base + k ns
 #pragma unroll
                 for (int k = 0; k < q; k++) lds[lds_at(LL, c, base + k * ns)] = comp ? v[u * q + k].im : v[u * q + k].re;
@@ -1027,7 +1035,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #pragma unroll
             for (int u = 0; u < Nx::U; u++) {
                 int c, b;
-                Nx::map(tid, u, c, b);
+                Nx::map(tidc, u, c, b);
 #pragma unroll
                 for (int k = 0; k < Nx::q; k++) {
                     const T x = lds[lds_at(LL, c, b + k * Nx::NB)];
