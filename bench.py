@@ -341,10 +341,10 @@ class Job:
                               stream=self.stream)
         self.y = torch.empty(self.desc["out_elems"], dtype=cdt, device=self.dev)
         # placement tuning before the warm-up (pifft_plan_tune_workspace: the
-        # fastest of 4 workspace allocations for this output; ~80 ms at 2^28,
+        # fastest of 8 workspace allocations for this output; ~0.2 s at 2^28,
         # profiles/r03_workspace_tuning.log: C4 4.62-4.81 -> 4.59-4.62 ms)
         self.tuned_ms = self.plan.tune_workspace(self.x.data_ptr(), self.y.data_ptr(), self.stream,
-                                                 int(os.environ.get("BENCH_W_TRIES", "4")))
+                                                 int(os.environ.get("BENCH_W_TRIES", "8")))
 
     def step(self):
         self.plan.execute_device(self.x.data_ptr(), self.y.data_ptr(), self.stream)
