@@ -164,7 +164,7 @@ def test_config5_all_workers_n2e32():
 @pytest.mark.timeout(600)
 def test_config4_fp32_full_size_vs_oracle():
     """The reference's own precision (data_t = float, CPU.c:33-36) at N = 2^28:
-    the default fp32 plan (three packed 32-value passes 1024 x 512 x 512) and
+    the default fp32 plan (three packed 32-value passes 512 x 512 x 1024) and
     the 8-worker plan against the oracle (fp32 restatement, 16 workers).
     Bar: rel-L2 <= 1e-5 log2 N."""
     n, logn = 1 << 28, 28
@@ -289,3 +289,42 @@ def test_packed_vpt32_fp32_three_pass_bitwise(pos, monkeypatch):
     v32.execute_device(x.data_ptr(), yb.data_ptr(), st)
     torch.cuda.synchronize()
     assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb))
+
+
+# shapes whose radix order the position-aware planner changed (round 3,
+# profiles/r03_pos_model_shapes.log): (log2 N, precision, workers)
+POS_SHAPES = [(25, pifft.F32, 1), (26, pifft.F32, 1), (25, pifft.F64, 64), (29, pifft.F64, 1)]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("logn,prec,P", POS_SHAPES)
+def test_position_model_orders_vs_oracle(logn, prec, P, monkeypatch):
+    """Every plan shape whose radix order the position model changed, in both
+    orders (PIFFT_POS_MODEL 1 / 0): the orders differ, and each result matches
+    the oracle (2^25-2^26) or, at 2^29, the other order's result, per bin.
+    Bars: rel-L2 <= 1e-12 fp64, <= 1e-5 log2 N fp32."""
+    n = 1 << logn
+    f64 = prec == pifft.F64
+    cdt = torch.complex128 if f64 else torch.complex64
+    tol = TOL64 if f64 else 1e-5 * logn
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=cdt, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, prec, seed=91, stream=st)
+    got, radix = {}, {}
+    for pos in ("1", "0"):
+        monkeypatch.setenv("PIFFT_POS_MODEL", pos)
+        plan = pifft.Plan(n, P, 1, prec)
+        radix[pos] = plan.describe()["radix"]
+        y = torch.empty_like(x)
+        plan.execute_device(x.data_ptr(), y.data_ptr(), st)
+        torch.cuda.synchronize()
+        got[pos] = y.cpu().numpy()
+        plan.close()
+        del y
+    assert radix["1"] != radix["0"], radix
+    if logn <= 26:
+        want = oracle.fft(x.cpu().numpy(), P=16, nthreads=_threads())
+        for g in got.values():
+            _check_bins(g, want, tol=tol)
+    else:
+        _check_bins(got["1"], got["0"], tol=tol)
