@@ -789,6 +789,18 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const PassKernel* fused = nullptr;
     if (may_fuse && passes.size() > 1)
         fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp);
+    // All P workers in the worker-interleaved layout: the tree fused into the
+    // first pass too (MODE 11 = 3 | 8).  A tile's lines are whole P-worker line
+    // blocks; each lane evaluates its own worker's path from the P leaves of
+    // its position, which the P lanes of one block load at one address -- the
+    // tree's write and the first pass's re-read of N values disappear.
+    // PIFFT_WIL_FUSE: 1 on; PIFFT_WIL_FUSE_C: lines per workgroup (tuning).
+    if (p->wil && !fused && !p->separate_tree && env_int("PIFFT_FUSE_TREE", 1) && env_int("PIFFT_WIL_FUSE", 0)) {
+        const int cf = env_int("PIFFT_WIL_FUSE_C", 0);
+        const int C = cf > 0 ? cf : passes[0].C;
+        fused = find_pass(p->prec, passes[0].R, C, 11, passes[0].nts, p->lp);
+        if (fused) passes[0].C = C;
+    }
     p->fused_tree = fused != nullptr;
 
     // --- chain: [tree] [passes] [interleave] ---
@@ -883,7 +895,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         if (fuse_here) {
             s.pa.tree = ttw;
             s.pa.worker = p->q0;
-            s.pa.log_nq = (uint32_t)ilog2u(p->nq);
+            s.pa.log_nq = p->wil ? 0u : (uint32_t)ilog2u(p->nq);  // (MODE 11: the workers are in the lines)
         }
         s.pa.out_bstride = M;
         s.pa.nlines = ntrans * (M >> logr);
@@ -918,7 +930,12 @@ int build_plan(pifft_plan* p, bool dry = false) {
                                                              (unsigned long long)(wgs * k->nt));
         s.grid = dim3((unsigned)wgs);
         s.lds = (size_t)k->lds_bytes;
-        s.bytes = fuse_here ? (uint64_t)p->batch * p->nq * (p->n + M) * esz : 2 * ntrans * M * esz;
+        // (a fused pass reads every leaf of its workers' transforms: all N
+        // once for a MODE 11 pass, whose P workers share them; N per worker
+        // for MODE 3)
+        s.bytes = !fuse_here ? 2 * ntrans * M * esz
+                  : p->wil   ? 2 * (uint64_t)p->batch * p->n * esz
+                             : (uint64_t)p->batch * p->nq * (p->n + M) * esz;
         if (s.lds > 65536 && !dry)
             (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {

@@ -840,8 +840,18 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 constexpr int G = P >= TL ? 1 : TL / P;
                 static_assert(q % G == 0, "whole rounds of leaf loads");
                 const uint32_t log_m = log_lb + Sh::LOGR;
+                // MODE 11 (= 3 | 8, all workers, worker-interleaved layout):
+                // launch line l = (jw << wil) + wq is worker wq's line jw; its
+                // leaves sit at jw + r M/R + m M of the transform's input, and
+                // the lanes of one jw (c-fast) load the same leaves (one
+                // address per P lanes) while each evaluates its own worker's
+                // path
+                const uint64_t jw = WIL ? (j >> wil) : j;
+                const uint32_t wq = WIL ? (uint32_t)(j & ((1ull << wil) - 1))
+                                        : a.worker + (uint32_t)(tile * C >> log_lb & ((1u << a.log_nq) - 1));
+                const C2* lsrc = WIL ? in + bin * a.in_bstride + jw + ((uint64_t)b << log_lb) : src;
                 // this thread's base twiddles w_N^{zi0 2^t}, zi0 = its k = 0 input
-                const uint64_t zi0 = j + ((uint64_t)b << log_lb);
+                const uint64_t zi0 = jw + ((uint64_t)b << log_lb);
                 C2 bt[LP];
 #pragma unroll
                 for (int t = 0; t < LP; t++) bt[t] = tree_tw_lv<T>(a.tree, zi0, t);
@@ -850,7 +860,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     C2 w[G][P];
 #pragma unroll
                     for (int g = 0; g < G; g++) {
-                        const C2* leaf = src + ((uint64_t)((k0 + g) * NB) << log_lb);
+                        const C2* leaf = lsrc + ((uint64_t)((k0 + g) * NB) << log_lb);
 #pragma unroll
                         for (int m = 0; m < P; m++)
                             w[g][m] = ok ? ld_stream<nt_loads(NTS)>(leaf + ((uint64_t)m << log_m)) : C2{(T)0, (T)0};
@@ -858,7 +868,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     static_for<0, G, 1>([&](auto gc) {
                         constexpr int g = decltype(gc)::value;
                         v[u * q + k0 + g] =
-                            tree_path_steps<T, LP, q, k0 + g>(w[g], bt, a.worker + (uint32_t)(tile * C >> log_lb & ((1u << a.log_nq) - 1)));
+                            tree_path_steps<T, LP, q, k0 + g>(w[g], bt, wq);
                     });
                     __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
                 });
@@ -1275,7 +1285,7 @@ template <typename T, int R, int C, int MODE, int LP, int VPT, int H>
 constexpr int pass_waves_per_eu() {
     constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
     if constexpr (H > 1) return w > 2 ? w / 2 : w;
-    else return (MODE == 3 && LP >= 4 && w > 2) ? 2 : w;
+    else return ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)

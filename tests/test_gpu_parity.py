@@ -764,6 +764,42 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
         assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
 
 
+@pytest.mark.parametrize("suf,logn,P,batch,cf", [("f64", 20, 8, 1, 0), ("f32", 20, 8, 3, 0), ("f64", 20, 16, 1, 0),
+                                                 ("f64", 22, 4, 1, 0), ("f64", 21, 8, 2, 16), ("f32", 23, 16, 1, 8),
+                                                 ("f64", 19, 8, 1, 32), ("f32", 18, 4, 2, 32)])
+def test_worker_interleaved_fused_tree_vs_oracle(suf, logn, P, batch, cf, monkeypatch):
+    """The tree fused into the first worker-interleaved pass (MODE 11,
+    PIFFT_WIL_FUSE=1; PIFFT_WIL_FUSE_C lines per workgroup): no tree launch,
+    each lane evaluating its own worker's path from leaves shared by the P
+    lanes of its line block.  Within tolerance of the oracle and of the
+    unfused plan (the fused path uses factored tree twiddles: not bitwise)."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn * 5 + P)
+    d_in = dev(x)
+    st = torch.cuda.current_stream()
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "1")
+    if cf:
+        monkeypatch.setenv("PIFFT_WIL_FUSE_C", str(cf))
+    fused = pifft.Plan(n, P, batch, PREC[suf])
+    d = fused.describe()
+    assert d["worker_interleaved"] and d["launch_kind"][0] == "tree+pass" and "tree" not in d["launch_kind"], d
+    if cf:
+        assert d["lines"][0] == cf
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")
+    plain = pifft.Plan(n, P, batch, PREC[suf])
+    assert plain.describe()["launch_kind"][0] == "tree"
+    a = torch.empty_like(d_in)
+    b = torch.empty_like(d_in)
+    fused.execute_device(d_in.data_ptr(), a.data_ptr(), st)
+    plain.execute_device(d_in.data_ptr(), b.data_ptr(), st)
+    torch.cuda.synchronize()
+    got, ref = a.cpu().numpy().reshape(batch, n), b.cpu().numpy().reshape(batch, n)
+    for bt in range(batch):
+        want = oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8)
+        assert_bins_close(got[bt], want, suf, n)
+        assert_bins_close(got[bt], ref[bt], suf, n)
+
+
 # ------------------------------------------------ the final exchange (8e) ---
 @pytest.mark.parametrize("suf,logn,P,per,batch", [("f64", 20, 8, 1, 1), ("f32", 18, 8, 2, 3), ("f64", 16, 4, 1, 2),
                                                   ("f64", 12, 64, 16, 1)])

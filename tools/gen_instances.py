@@ -4,7 +4,8 @@ spread over NPART translation units (compiled in parallel).
 
 Rules: NT = C*R/VPT threads (VPT = 16 values per thread) <= 1024; LDS = C*(R + R/16 + 1)*sizeof(T)
 <= 160 KiB.  MODE 0 single pass (any C); MODE 1/2 strided passes (C >= 4);
-MODE 10 = MODE 2 on the worker-interleaved layout (all-worker plans).
+MODE 10 = MODE 2 on the worker-interleaved layout (all-worker plans); MODE 11 =
+MODE 3 on it (the tree fused into an all-worker plan's first pass).
 MODE 3 = MODE 1 with the tree fused in, LP = log2 P in 1..4, at the planner's
 tile (8192 elements, both precisions) and C = 4.  MODE 4 / 6 = MODE 0 / 2
 storing in bit-reversed order (the last pass of a PIFFT_OUT_BITREV plan), for
@@ -63,6 +64,17 @@ for T, prec in (("double", 64), ("float", 32)):
             for nts in (0, 1):
                 for lp in (1, 2, 3, 4):
                     items.append(f"PK({T}, {prec}, {R}, {C}, 3, {nts}, {lp}),")
+# MODE 11 = 3 | 8: the tree fused into the first pass of an all-worker plan in
+# the worker-interleaved layout (PIFFT_WIL_FUSE), P = 4..16, C >= 8 lines (a
+# whole number of P-worker line blocks) at tiles of <= 8192 values
+for T, prec in (("double", 64), ("float", 32)):
+    for R in (128, 256, 512, 1024):
+        for C in (8, 16, 32, 64):
+            if R * C > 8192:
+                continue
+            for nts in (0, 1):
+                for lp in (2, 3, 4):
+                    items.append(f"PK({T}, {prec}, {R}, {C}, 11, {nts}, {lp}),")
 # two sub-tiles per workgroup (k_pass H = 2, one workgroup per CU): the
 # 2^28 three-pass plans' strided passes with twice the lines per workgroup on
 # the read side (PIFFT_SUBTILES)
