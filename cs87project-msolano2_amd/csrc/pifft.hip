@@ -128,7 +128,7 @@ const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int l
 // plan
 // ---------------------------------------------------------------------------
 enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4, STEP_CHUNK_A = 5, STEP_CHUNK_B = 6 };
-enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, BUF_CH = 5, NBUF = 6 };
+enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, BUF_CH = 5, BUF_W2 = 6, NBUF = 7 };
 
 struct Step {
     int kind = 0;
@@ -166,7 +166,7 @@ struct pifft_plan {
     int prof_steps = 0, prof_used = 0, prof_mode = 0;
     int radix[8] = {0}, lines[8] = {0}, vpt[8] = {0};
     void* buf[NBUF] = {nullptr};
-    size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0, bytes_ch = 0;
+    size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0, bytes_ch = 0, bytes_w2 = 0;
     int chunk_pairs = 0;  // chunked last-two-pass pairs (one per chunk)
     void* d_tw = nullptr;
     size_t tw_bytes = 0;
@@ -967,10 +967,15 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // destinations, backwards: last -> OUT, then W, OUT, W, ...
     std::vector<int> dst(chain.size());
     for (size_t i = chain.size(); i-- > 0;) dst[i] = ((chain.size() - 1 - i) % 2 == 0) ? BUF_OUT : BUF_W;
-    bool need_w = false;
+    // tuning (PIFFT_W2=1): an odd chain of >= 3 elements writes its first
+    // element into a second workspace instead of the caller's output, so the
+    // output is touched only by the last pass (x -> W2 -> W -> out)
+    if (env_int("PIFFT_W2", 0) && chain.size() >= 3 && dst[0] == BUF_OUT) dst[0] = BUF_W2;
+    bool need_w = false, need_w2 = false;
     for (size_t i = 0; i < chain.size(); i++) {
         const int src = (i == 0) ? BUF_IN : dst[i - 1];
         if (dst[i] == BUF_W || src == BUF_W) need_w = true;
+        if (dst[i] == BUF_W2) need_w2 = true;
         for (auto& s : chain[i].steps) {
             if (s.src == -1) s.src = src;
             if (s.dst == -2) s.dst = dst[i];
@@ -989,14 +994,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // at 512 MiB (fp64 2^25, the worker of 8 at 2^28) padding cost 1.5-2.5 %,
     // at 1 GiB it ties, at 2 GiB (the worker of 2 at 2^28, of 8 at 2^30) it
     // gains ~0.5 % (profiles/r02_wpad.log, tools/gpu_wpad_shapes.sh).
-    uint64_t w_tr = M;  // elements per transform in W
+    uint64_t w_tr = M, w2_tr = M;  // elements per transform in W, W2
     const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));
     const uint64_t w_min = (uint64_t)env_int("PIFFT_W_PAD_MIN_MIB", 2048) << 20;
     if (w_pad && !p->wil && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
         for (size_t i = 0; i + 1 < p->steps.size(); i++) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
-            if (a.dst != BUF_W || b.src != BUF_W || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
+            if (a.dst != b.src || (a.dst != BUF_W && a.dst != BUF_W2) || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
                 b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log ||
                 a.nts == 2 || a.nts == 3 || b.nts == 2 || b.nts == 3)  // chunked-pair instances: unpadded only
                 continue;
@@ -1006,10 +1011,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
             a.pa.out_pad = b.pa.in_pad = (uint32_t)w_pad;
             a.pa.out_pad_log = b.pa.log_lb - logr_a;
             a.pa.out_bstride = b.pa.in_bstride = tr;
-            w_tr = std::max(w_tr, tr);
+            if (a.dst == BUF_W2)
+                w2_tr = std::max(w2_tr, tr);
+            else
+                w_tr = std::max(w_tr, tr);
         }
     }
     p->bytes_w = need_w ? (size_t)p->batch * p->nq * w_tr * esz : 0;
+    p->bytes_w2 = need_w2 ? (size_t)p->batch * p->nq * w2_tr * esz : 0;
     if (dry) return 0;
     // tuning knob (tools/probe_place.py): hipExtMallocWithFlags flags for the
     // ping-pong workspace, e.g. 4 = hipDeviceMallocContiguous
@@ -1017,6 +1026,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     if (p->bytes_w)
         HIPCHK(w_flags ? hipExtMallocWithFlags(&p->buf[BUF_W], p->bytes_w, (unsigned)w_flags)
                        : hipMalloc(&p->buf[BUF_W], p->bytes_w));
+    if (p->bytes_w2) HIPCHK(hipMalloc(&p->buf[BUF_W2], p->bytes_w2));
     if (p->bytes_ta) HIPCHK(hipMalloc(&p->buf[BUF_TA], p->bytes_ta));
     if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
     if (p->bytes_ch) HIPCHK(hipMalloc(&p->buf[BUF_CH], p->bytes_ch));
@@ -1084,7 +1094,8 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
 // (round-2 verdict); kernel-bound events add nothing to the stream.
 int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hipStream_t st,
                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
-    void* base[NBUF] = {const_cast<void*>(d_in), d_out, p->buf[BUF_W], p->buf[BUF_TA], p->buf[BUF_TB], p->buf[BUF_CH]};
+    void* base[NBUF] = {const_cast<void*>(d_in), d_out,           p->buf[BUF_W], p->buf[BUF_TA],
+                        p->buf[BUF_TB],             p->buf[BUF_CH], p->buf[BUF_W2]};
     const char* src = (const char*)base[s.src] + s.src_off * p->esz;
     char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
     auto go = [&](void** args, size_t lds) {
@@ -1398,7 +1409,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     info->local_n = p->m;
     info->in_elems = (uint64_t)p->batch * p->n;
     info->out_elems = out_elems(p);
-    info->workspace_bytes = p->bytes_w + p->bytes_ta + p->bytes_tb + p->bytes_ch + p->tw_bytes;
+    info->workspace_bytes = p->bytes_w + p->bytes_w2 + p->bytes_ta + p->bytes_tb + p->bytes_ch + p->tw_bytes;
     info->chunk_pairs = p->chunk_pairs;
     info->layout = (p->wil ? 1 : 0) | (p->ilv ? 2 : 0);
     info->num_launches = (int)p->steps.size();
