@@ -58,7 +58,16 @@ int fail(const char* fmt, ...) {
         if (e_ != hipSuccess) return fail("%s failed: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
+// Planner tuning variables (PIFFT_* below) are read only when PIFFT_TUNING=1
+// is set: a variable inherited from a shell never changes the product's plan
+// (tests/test_planner.py::test_stray_tuning_variables_are_ignored).  Each
+// default is the measured winner cited where it is read.
+bool tuning_on() {
+    const char* s = getenv("PIFFT_TUNING");
+    return s && s[0] == '1' && s[1] == 0;
+}
 int env_int(const char* name, int dflt) {
+    if (!tuning_on()) return dflt;
     const char* s = getenv(name);
     return (s && *s) ? atoi(s) : dflt;
 }
@@ -116,10 +125,9 @@ const std::vector<PassKernel>& pass_kernels() {
     return all;
 }
 
-const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0, int vpt = 16, int h = 1) {
+const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0, int vpt = 16) {
     for (const auto& k : pass_kernels())
-        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt &&
-            k.h == h)
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt)
             return &k;
     return nullptr;
 }
@@ -127,8 +135,8 @@ const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int l
 // ---------------------------------------------------------------------------
 // plan
 // ---------------------------------------------------------------------------
-enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4, STEP_CHUNK_A = 5, STEP_CHUNK_B = 6 };
-enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, BUF_TB = 4, BUF_CH = 5, BUF_W2 = 6, NBUF = 7 };
+enum { STEP_TREE = 1, STEP_PASS = 2, STEP_INTERLEAVE = 3, STEP_TREE_PASS = 4 };
+enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, NBUF = 4 };
 
 struct Step {
     int kind = 0;
@@ -138,7 +146,7 @@ struct Step {
     int src = -1, dst = -2;  // -1 / -2: the chain element's input / output buffer
     uint64_t src_off = 0, dst_off = 0;  // elements
     PassArgs pa{};
-    int nts = 0;  // STEP_PASS / STEP_TREE_PASS: the instance's streaming form (2, 3: chunked-pair instances)
+    int nts = 0;  // STEP_PASS / STEP_TREE_PASS: the instance's streaming form
     TreeArgs ta{};
     uint64_t il_total = 0;
     uint32_t il_log_n = 0, il_log_p = 0;
@@ -166,8 +174,7 @@ struct pifft_plan {
     int prof_steps = 0, prof_used = 0, prof_mode = 0;
     int radix[8] = {0}, lines[8] = {0}, vpt[8] = {0};
     void* buf[NBUF] = {nullptr};
-    size_t bytes_w = 0, bytes_ta = 0, bytes_tb = 0, bytes_ch = 0, bytes_w2 = 0;
-    int chunk_pairs = 0;  // chunked last-two-pass pairs (one per chunk)
+    size_t bytes_w = 0, bytes_ta = 0;
     void* d_tw = nullptr;
     size_t tw_bytes = 0;
     hipStream_t stream = nullptr;
@@ -288,7 +295,6 @@ uint64_t interleave_threads(uint64_t total, int lp, int prec, uint64_t n) {
 struct PassChoice {
     int R, C, mode, nts;
     int vpt = 16;
-    int h = 1;  // sub-tiles per workgroup (k_pass H)
 };
 
 // Tile = R x C elements per workgroup (C adjacent lines of an R-point sub-FFT).
@@ -421,7 +427,7 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
     }
     // tuning: explicit log2 radices, e.g. PIFFT_RADIX_LOGS=10,10,8 (must sum to log2 M)
     bool explicit_radices = false;
-    if (const char* rl = getenv("PIFFT_RADIX_LOGS")) {
+    if (const char* rl = tuning_on() ? getenv("PIFFT_RADIX_LOGS") : nullptr) {
         std::vector<int> logs;
         for (const char* c = rl; *c;) {
             char* end = nullptr;
@@ -508,20 +514,6 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         }
     }
     if (out.empty()) return fail("no pass decomposition for M=2^%d", logm);
-    // tuning: two sub-tiles per workgroup on the strided passes (k_pass H = 2,
-    // one workgroup per CU): PIFFT_SUBTILES=2 (every strided pass),
-    // PIFFT_SUBTILES_FIRST=2 (the first pass only) or PIFFT_SUBTILES_LAST=2
-    // (the last pass only)
-    {
-        const int hall = env_int("PIFFT_SUBTILES", 1), hfirst = env_int("PIFFT_SUBTILES_FIRST", hall);
-        const int hlast = env_int("PIFFT_SUBTILES_LAST", hall);
-        for (size_t i = 0; i < out.size(); i++) {
-            PassChoice& pc = out[i];
-            const bool last = i + 1 == out.size() && out.size() > 1;
-            const int h = (pc.mode == 1) ? hfirst : (pc.mode == 2 ? (last ? hlast : hall) : 1);
-            if (h > 1 && find_pass(prec, pc.R, pc.C, pc.mode, pc.nts, 0, pc.vpt, h)) pc.h = h;
-        }
-    }
     // the packed VPT-32 passes for the 16384-value tile (every strided pass
     // must have its instance, else the plan is redone at the 8192 tile)
     if (v32) {
@@ -562,104 +554,15 @@ struct Elem {
     std::vector<Step> steps;
 };
 
-// The last two passes (a, b) of a plan of >= 3 passes whose data exceed the
-// Infinity Cache, run as chunked pairs (PassArgs: line map, virtual sides):
-// per chunk, pass a streams its inputs from HBM (nt loads) into a scratch
-// buffer of PIFFT_CHUNK_MIB MiB with plain stores, and pass b reads the
-// scratch back -- from the Infinity Cache -- and streams its outputs to HBM
-// (nt stores).  Off by default: measured on MI355X (profiles/r01_tune_chunked
-// .log) the pair runs at the same per-pass rate from the cache as from HBM
-// (C4 at 128 MiB chunks: 4.72 vs 4.81-4.84 ms, within box drift; the 8-way
-// split at 2^28 loses 6-20 %), i.e. the passes are bound by their own
-// load/exchange/store pipeline near 5.2-5.8 TB/s, not by HBM.  A chunk is W consecutive residues d < L = M/(Ra Rb) of
-// one transform, or, when a whole transform fits, a group of transforms.
-// Replaces the chain's last two elements with one.
-int chunk_last_two(pifft_plan* p, const std::vector<PassChoice>& passes, std::vector<Elem>& chain, bool dry) {
-    const int chunk_mib = env_int("PIFFT_CHUNK_MIB", 0);
-    const size_t k = passes.size();
-    if (chunk_mib <= 0 || k < 3 || p->bitrev || p->ilv || chain.size() < 2) return 0;
-    const PassChoice &ca = passes[k - 2], &cb = passes[k - 1];
-    if (ca.mode != 2 || cb.mode != 2 || ca.nts != 1 || cb.nts != 1) return 0;
-    const PassKernel* ka = find_pass(p->prec, ca.R, ca.C, 2, 2);
-    const PassKernel* kb = find_pass(p->prec, cb.R, cb.C, 2, 3);
-    if (!ka || !kb) return 0;
-    const Step sa = chain[chain.size() - 2].steps.at(0), sb = chain[chain.size() - 1].steps.at(0);
-    if (sa.kind != STEP_PASS || sb.kind != STEP_PASS) return 0;
-    const uint64_t M = p->m, ntrans = (uint64_t)p->batch * p->nq;
-    const uint64_t Ra = (uint64_t)ca.R, Rb = (uint64_t)cb.R, L = M / (Ra * Rb);
-    const uint64_t ce = ((uint64_t)chunk_mib << 20) / p->esz;  // chunk elements
-    Elem e;
-    auto add = [&](Step s, const PassKernel* kk, int kind, uint64_t nlines) {
-        s.kind = kind;
-        s.fn = kk->fn;
-        s.pa.nlines = nlines;
-        s.grid = dim3((unsigned)((nlines + kk->C - 1) / kk->C));
-        s.bytes = 2 * nlines * (uint64_t)kk->R * p->esz;
-        e.steps.push_back(s);
-    };
-    if (M <= ce) {
-        // whole transforms: groups of G through the scratch, unchanged addressing
-        const uint64_t G = ce / M;
-        if (ntrans < 2) return 0;  // the whole job fits the Infinity Cache anyway
-        for (uint64_t g0 = 0; g0 < ntrans; g0 += G) {
-            const uint64_t gi = std::min(G, ntrans - g0);
-            Step a = sa, b = sb;
-            a.src_off = g0 * M;
-            a.dst = BUF_CH;
-            a.src = -1;
-            b.src = BUF_CH;
-            b.dst_off = g0 * M;
-            add(a, ka, STEP_CHUNK_A, gi * (M / Ra));
-            add(b, kb, STEP_CHUNK_B, gi * (M / Rb));
-        }
-        p->bytes_ch = (size_t)std::min(G, ntrans) * M * p->esz;
-    } else {
-        uint64_t W = ce / (Ra * Rb);
-        if (W < (uint64_t)std::max(ka->C, kb->C) || W >= L) return 0;
-        const uint32_t log_w = (uint32_t)ilog2u(W), log_l = (uint32_t)ilog2u(L);
-        if (ntrans * (L / W) * 2 > PIFFT_MAX_LAUNCH_INFO - 16) return 0;
-        for (uint64_t bt = 0; bt < ntrans; bt++) {
-            for (uint64_t d0 = 0; d0 < L; d0 += W) {
-                Step a = sa, b = sb;
-                a.src_off = bt * M;
-                a.dst = BUF_CH;
-                a.pa.d0 = b.pa.d0 = d0;
-                a.pa.wmask = b.pa.wmask = W - 1;
-                a.pa.log_sh = b.pa.log_sh = log_l - log_w;
-                // pass a: global reads; stores as a transform of W Ra Rb points (Ns = W)
-                a.pa.wr_virt = 1;
-                a.pa.out_log_ns = log_w;
-                // pass b: reads that transform (line stride W Ra); global stores
-                b.src = BUF_CH;
-                b.dst_off = bt * M;
-                b.pa.rd_virt = 1;
-                b.pa.in_log_es = log_w + (uint32_t)ilog2u(Ra);
-                add(a, ka, STEP_CHUNK_A, W * Rb);
-                add(b, kb, STEP_CHUNK_B, W * Ra);
-            }
-        }
-        p->bytes_ch = (size_t)W * Ra * Rb * p->esz;
-    }
-    for (auto& s : e.steps)
-        if (s.lds > 65536 && !dry) (void)hipFuncSetAttribute(s.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
-    p->chunk_pairs = (int)(e.steps.size() / 2);
-    chain.pop_back();
-    chain.pop_back();
-    chain.push_back(e);
-    return 0;
-}
-
 // dry: plan only (pifft_plan_dry_run) -- no device, no allocation
 int build_plan(pifft_plan* p, bool dry = false) {
     const size_t esz = p->esz;
     const uint64_t ntrans = (uint64_t)p->batch * p->nq;  // local transforms
     std::vector<PassChoice> passes;
-    // One worker per plan: the fused pass reads the input once.  Several
-    // workers (the whole transform on one GPU, small N): each worker's pass
-    // re-reads all P leaves, P x the input, which pays only while the input
-    // stays in the Infinity Cache -- PIFFT_FUSE_ALL_MAX_MIB of input
-    // (measured, profiles/r02_fuse_all.log: no consistent win, off by default)
-    const uint64_t in_mib = ((uint64_t)p->batch * p->n * esz) >> 20;
+    // One worker per plan: the tree is fused into the first pass, which reads
+    // the input once.  (Several workers per plan re-reading all P leaves in
+    // each worker's fused pass measured no consistent win, profiles/
+    // r02_fuse_all.log; removed in round 4.)
     // All P <= 16 workers of a natural-order plan on this GPU, with a
     // multi-pass local FFT: the worker-interleaved layout (PassArgs::wil).
     // The tree's one launch writes z_q[i] at i P + q, every pass reads and
@@ -667,11 +570,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // stores worker q at slot bitrev(q) -- the natural-order result, without
     // an interleave launch or scattered 16-B stores.  PIFFT_WORKER_IL=0: the
     // slice-major layout (+ interleave launch or natural-order store).
-    const bool wil_ok = p->natural && p->P > 1 && p->nq == p->P && p->lp <= 4 && env_int("PIFFT_WORKER_IL", 1) &&
-                        env_int("PIFFT_CHUNK_MIB", 0) <= 0;
-    const bool fuse_all = !wil_ok && p->nq > 1 && in_mib < (uint64_t)env_int("PIFFT_FUSE_ALL_MAX_MIB", 0);
-    const bool may_fuse = p->P > 1 && (p->nq == 1 || fuse_all) && p->lp <= 4 && !p->separate_tree &&
-                          env_int("PIFFT_FUSE_TREE", 1);
+    const bool wil_ok = p->natural && p->P > 1 && p->nq == p->P && p->lp <= 4 && env_int("PIFFT_WORKER_IL", 1);
+    const bool may_fuse = p->P > 1 && p->nq == 1 && p->lp <= 4 && !p->separate_tree && env_int("PIFFT_FUSE_TREE", 1);
     if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0, true, !wil_ok)) return -1;
     if (wil_ok && passes.size() > 1) {
         // the same radices, every pass a worker-interleaved MODE 2 (| 8)
@@ -684,7 +584,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
                               p->prec == 64 ? "PIFFT_COL_C64" : "PIFFT_COL_C32", 2);
             pc.mode = 2 | 8;
             pc.vpt = 16;
-            pc.h = 1;
             // tuning: at least this many lines per workgroup (e.g. P, so a
             // row holds every worker's value), if instantiated
             // (default P: 8 workers at C = 8 instead of 4 -- C2 35 -> 32 us,
@@ -710,7 +609,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
             return fail("no bit-reversed pass kernel R=%d C=%d mode=%d", l.R, l.C, bm);
         l.C = C;
         l.mode = bm | 4;
-        l.h = 1;
     }
 
     // All P workers on this plan, natural order, and an output small enough to
@@ -725,8 +623,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // PIFFT_ILV: -1 this rule, 0 never, 1 always (where it applies).
     {
         const int force = env_int("PIFFT_ILV", -1);
-        const bool ok = p->natural && p->P > 1 && p->nq == p->P && !passes.empty() && !p->wil &&
-                        env_int("PIFFT_CHUNK_MIB", 0) <= 0;
+        const bool ok = p->natural && p->P > 1 && p->nq == p->P && !passes.empty() && !p->wil;
         bool on = ok && force == 1;
         if (ok && force < 0) {
             const PassChoice& l = passes.back();
@@ -739,10 +636,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
         p->ilv = on;
     }
-    if (p->ilv) {
-        passes.back().nts = 0;
-        passes.back().h = 1;
-    }
+    if (p->ilv) passes.back().nts = 0;
     TableBuilder tb(esz);
     // --- tree tables (w_N) ---
     const bool need_tree = p->P > 1;
@@ -789,18 +683,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const PassKernel* fused = nullptr;
     if (may_fuse && passes.size() > 1)
         fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp);
-    // All P workers in the worker-interleaved layout: the tree fused into the
-    // first pass too (MODE 11 = 3 | 8).  A tile's lines are whole P-worker line
-    // blocks; each lane evaluates its own worker's path from the P leaves of
-    // its position, which the P lanes of one block load at one address -- the
-    // tree's write and the first pass's re-read of N values disappear.
-    // PIFFT_WIL_FUSE: 1 on; PIFFT_WIL_FUSE_C: lines per workgroup (tuning).
-    if (p->wil && !fused && !p->separate_tree && env_int("PIFFT_FUSE_TREE", 1) && env_int("PIFFT_WIL_FUSE", 0)) {
-        const int cf = env_int("PIFFT_WIL_FUSE_C", 0);
-        const int C = cf > 0 ? cf : passes[0].C;
-        fused = find_pass(p->prec, passes[0].R, C, 11, passes[0].nts, p->lp);
-        if (fused) passes[0].C = C;
-    }
     p->fused_tree = fused != nullptr;
 
     // --- chain: [tree] [passes] [interleave] ---
@@ -879,8 +761,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         const int last_nt = last_pass && passes[i].mode == 2 ? env_int("PIFFT_LAST_NT", -1) : -1;
         const PassKernel* k = fuse_here ? fused
                                         : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode,
-                                                    last_nt >= 0 ? last_nt : passes[i].nts, 0, passes[i].vpt,
-                                                    passes[i].h);
+                                                    last_nt >= 0 ? last_nt : passes[i].nts, 0, passes[i].vpt);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
@@ -895,7 +776,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         if (fuse_here) {
             s.pa.tree = ttw;
             s.pa.worker = p->q0;
-            s.pa.log_nq = p->wil ? 0u : (uint32_t)ilog2u(p->nq);  // (MODE 11: the workers are in the lines)
+            s.pa.log_nq = (uint32_t)ilog2u(p->nq);
         }
         s.pa.out_bstride = M;
         s.pa.nlines = ntrans * (M >> logr);
@@ -905,12 +786,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.log_xg = (uint32_t)env_int((passes[i].mode & 3) == 0 ? "PIFFT_XCD_GROUP_SINGLE" : "PIFFT_XCD_GROUP",
                                         (passes[i].mode & 3) == 0 ? 0 : 2);
         if (last_pass) s.pa.log_xg = (uint32_t)env_int("PIFFT_LAST_XCD_GROUP", (int)s.pa.log_xg);
-        s.pa.d0 = 0;  // identity line map, no virtual side (see PassArgs)
-        s.pa.wmask = ~0ull;
-        s.pa.log_sh = 0;
-        s.pa.rd_virt = s.pa.wr_virt = 0;
-        s.pa.in_log_es = s.pa.log_lb;
-        s.pa.out_log_ns = s.pa.log_ns;
         if (p->wil) {
             s.pa.wil = (uint32_t)p->lp;
             s.pa.wbrev = (i + 1 == passes.size()) ? 1u : 0u;  // the last pass: natural order
@@ -922,25 +797,18 @@ int build_plan(pifft_plan* p, bool dry = false) {
             s.pa.log_xg = std::max<uint32_t>(s.pa.log_xg, (uint32_t)env_int("PIFFT_ILV_XCD_GROUP", p->lp));
         }
         s.block = dim3((unsigned)k->nt);
-        const uint64_t lines_per_wg = (uint64_t)k->C * k->h;  // H sub-tiles of C lines
-        if (k->h > 1 && (s.pa.nlines % lines_per_wg || s.pa.ilv_log))
-            return fail("sub-tiled pass needs whole workgroups and no natural-order store");
-        const uint64_t wgs = (s.pa.nlines + lines_per_wg - 1) / lines_per_wg;
+        const uint64_t wgs = (s.pa.nlines + (uint64_t)k->C - 1) / (uint64_t)k->C;
         if (wgs * (uint64_t)k->nt >= (1ull << 32)) return fail("transform too large for one launch (%llu work-items)",
                                                              (unsigned long long)(wgs * k->nt));
         s.grid = dim3((unsigned)wgs);
         s.lds = (size_t)k->lds_bytes;
-        // (a fused pass reads every leaf of its workers' transforms: all N
-        // once for a MODE 11 pass, whose P workers share them; N per worker
-        // for MODE 3)
-        s.bytes = !fuse_here ? 2 * ntrans * M * esz
-                  : p->wil   ? 2 * (uint64_t)p->batch * p->n * esz
-                             : (uint64_t)p->batch * p->nq * (p->n + M) * esz;
+        // (a fused pass reads every leaf of its worker's transform: N per worker)
+        s.bytes = !fuse_here ? 2 * ntrans * M * esz : (uint64_t)p->batch * p->nq * (p->n + M) * esz;
         if (s.lds > 65536 && !dry)
             (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {
             p->radix[i] = k->R;
-            p->lines[i] = k->C * k->h;
+            p->lines[i] = k->C;
             p->vpt[i] = k->vpt;
         }
         ns *= (uint64_t)k->R;
@@ -948,7 +816,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
         e.steps.push_back(s);
         chain.push_back(e);
     }
-    if (chunk_last_two(p, passes, chain, dry)) return -1;
     if (p->natural && p->P > 1 && !p->ilv && !p->wil) {
         Step s;
         s.kind = STEP_INTERLEAVE;
@@ -967,15 +834,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // destinations, backwards: last -> OUT, then W, OUT, W, ...
     std::vector<int> dst(chain.size());
     for (size_t i = chain.size(); i-- > 0;) dst[i] = ((chain.size() - 1 - i) % 2 == 0) ? BUF_OUT : BUF_W;
-    // tuning (PIFFT_W2=1): an odd chain of >= 3 elements writes its first
-    // element into a second workspace instead of the caller's output, so the
-    // output is touched only by the last pass (x -> W2 -> W -> out)
-    if (env_int("PIFFT_W2", 0) && chain.size() >= 3 && dst[0] == BUF_OUT) dst[0] = BUF_W2;
-    bool need_w = false, need_w2 = false;
+    bool need_w = false;
     for (size_t i = 0; i < chain.size(); i++) {
         const int src = (i == 0) ? BUF_IN : dst[i - 1];
         if (dst[i] == BUF_W || src == BUF_W) need_w = true;
-        if (dst[i] == BUF_W2) need_w2 = true;
         for (auto& s : chain[i].steps) {
             if (s.src == -1) s.src = src;
             if (s.dst == -2) s.dst = dst[i];
@@ -994,16 +856,15 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // at 512 MiB (fp64 2^25, the worker of 8 at 2^28) padding cost 1.5-2.5 %,
     // at 1 GiB it ties, at 2 GiB (the worker of 2 at 2^28, of 8 at 2^30) it
     // gains ~0.5 % (profiles/r02_wpad.log, tools/gpu_wpad_shapes.sh).
-    uint64_t w_tr = M, w2_tr = M;  // elements per transform in W, W2
+    uint64_t w_tr = M;  // elements per transform in W
     const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));
     const uint64_t w_min = (uint64_t)env_int("PIFFT_W_PAD_MIN_MIB", 2048) << 20;
     if (w_pad && !p->wil && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
         for (size_t i = 0; i + 1 < p->steps.size(); i++) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
-            if (a.dst != b.src || (a.dst != BUF_W && a.dst != BUF_W2) || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
-                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log ||
-                a.nts == 2 || a.nts == 3 || b.nts == 2 || b.nts == 3)  // chunked-pair instances: unpadded only
+            if (a.dst != b.src || a.dst != BUF_W || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
+                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log)
                 continue;
             const uint64_t rows = M >> b.pa.log_lb;  // the reading pass's radix
             const uint64_t tr = M + rows * w_pad;
@@ -1011,14 +872,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
             a.pa.out_pad = b.pa.in_pad = (uint32_t)w_pad;
             a.pa.out_pad_log = b.pa.log_lb - logr_a;
             a.pa.out_bstride = b.pa.in_bstride = tr;
-            if (a.dst == BUF_W2)
-                w2_tr = std::max(w2_tr, tr);
-            else
-                w_tr = std::max(w_tr, tr);
+            w_tr = std::max(w_tr, tr);
         }
     }
     p->bytes_w = need_w ? (size_t)p->batch * p->nq * w_tr * esz : 0;
-    p->bytes_w2 = need_w2 ? (size_t)p->batch * p->nq * w2_tr * esz : 0;
     if (dry) return 0;
     // tuning knob (tools/probe_place.py): hipExtMallocWithFlags flags for the
     // ping-pong workspace, e.g. 4 = hipDeviceMallocContiguous
@@ -1026,10 +883,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     if (p->bytes_w)
         HIPCHK(w_flags ? hipExtMallocWithFlags(&p->buf[BUF_W], p->bytes_w, (unsigned)w_flags)
                        : hipMalloc(&p->buf[BUF_W], p->bytes_w));
-    if (p->bytes_w2) HIPCHK(hipMalloc(&p->buf[BUF_W2], p->bytes_w2));
     if (p->bytes_ta) HIPCHK(hipMalloc(&p->buf[BUF_TA], p->bytes_ta));
-    if (p->bytes_tb) HIPCHK(hipMalloc(&p->buf[BUF_TB], p->bytes_tb));
-    if (p->bytes_ch) HIPCHK(hipMalloc(&p->buf[BUF_CH], p->bytes_ch));
     HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->ev.resize(2 * p->steps.size());
     for (auto& e : p->ev) HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
@@ -1094,8 +948,7 @@ int create(pifft_plan** out, uint64_t n, uint32_t workers, uint32_t first, uint3
 // (round-2 verdict); kernel-bound events add nothing to the stream.
 int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hipStream_t st,
                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
-    void* base[NBUF] = {const_cast<void*>(d_in), d_out,           p->buf[BUF_W], p->buf[BUF_TA],
-                        p->buf[BUF_TB],             p->buf[BUF_CH], p->buf[BUF_W2]};
+    void* base[NBUF] = {const_cast<void*>(d_in), d_out, p->buf[BUF_W], p->buf[BUF_TA]};
     const char* src = (const char*)base[s.src] + s.src_off * p->esz;
     char* dst = (char*)base[s.dst] + s.dst_off * p->esz;
     auto go = [&](void** args, size_t lds) {
@@ -1105,9 +958,7 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
     hipError_t e = hipSuccess;
     switch (s.kind) {
         case STEP_PASS:
-        case STEP_TREE_PASS:
-        case STEP_CHUNK_A:
-        case STEP_CHUNK_B: {
+        case STEP_TREE_PASS: {
             PassArgs a = s.pa;
             a.in = src;
             a.out = dst;
@@ -1409,8 +1260,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     info->local_n = p->m;
     info->in_elems = (uint64_t)p->batch * p->n;
     info->out_elems = out_elems(p);
-    info->workspace_bytes = p->bytes_w + p->bytes_w2 + p->bytes_ta + p->bytes_tb + p->bytes_ch + p->tw_bytes;
-    info->chunk_pairs = p->chunk_pairs;
+    info->workspace_bytes = p->bytes_w + p->bytes_ta + p->tw_bytes;
     info->layout = (p->wil ? 1 : 0) | (p->ilv ? 2 : 0);
     info->num_launches = (int)p->steps.size();
     info->num_passes = p->npasses;

@@ -158,11 +158,9 @@ __device__ __forceinline__ void dft(cx<T>* v) {
 #ifndef PIFFT_NT_STORES
 #define PIFFT_NT_STORES 1
 #endif
-// NT (k_pass template argument): 0 plain; 1 nt loads and stores; 2 nt loads
-// only; 3 nt stores only (2/3: the two halves of a chunked pass pair whose
-// intermediate stays in the Infinity Cache, see PassArgs)
-constexpr bool nt_loads(int nt) { return nt == 1 || nt == 2; }
-constexpr bool nt_stores(int nt) { return nt == 1 || nt == 3; }
+// NTS (k_pass template argument): 0 plain; 1 nt loads and stores
+constexpr bool nt_loads(int nt) { return nt == 1; }
+constexpr bool nt_stores(int nt) { return nt == 1; }
 // PIFFT_VEC_NT: a complex value moves as ONE 8- or 16-byte vector access
 // (1: both precisions, 2: fp32 only, 0: two scalar nt accesses, which the
 // compiler merges -- for fp32 into loads that waited on each other).
@@ -441,24 +439,6 @@ struct PassArgs {
     // log_xg = g > 0, 2^g consecutive tiles (adjacent line groups) are given
     // to blocks of one XCD.  Needs gridDim.x % (8 << g) == 0 (else identity).
     uint32_t log_xg;
-    // Line map and virtual sides (chunked pass pairs).  The last two passes
-    // (radices Ra, Rb; L = M/(Ra Rb) = Ns of the first) split into L
-    // independent residue classes d: pass-a lines d + s L (s < Rb) feed
-    // exactly pass-b lines d + r L (r < Ra).  A chunk of W consecutive
-    // residues from d0 runs pass a into a scratch buffer small enough to stay
-    // in the Infinity Cache, then pass b out of it: HBM sees one read and one
-    // write of the data for the two passes.  Launch line l (< W * lines per
-    // residue) is global line j = d0 + (l & wmask) + ((l & ~wmask) << log_sh)
-    // (log_sh = log L - log W); the twiddles always use j.  A virtual side
-    // addresses the scratch with l as the line index of a transform of
-    // W Ra Rb points (rd_virt: element stride 2^in_log_es; wr_virt: Stockham
-    // store with Ns = 2^out_log_ns).  Unchunked passes: d0 = 0, wmask = ~0,
-    // log_sh = 0, no virtual side, in_log_es = log_lb, out_log_ns = log_ns.
-    uint64_t d0;
-    uint64_t wmask;
-    uint32_t log_sh;
-    uint32_t rd_virt, wr_virt;
-    uint32_t in_log_es, out_log_ns;
     // Natural-order store of a plan holding all P = 2^ilv_log workers (its
     // last pass; 0: the usual slice-major store).  Local transform bt is worker
     // bt mod P of batch bt / P, and its bin k lands at bitrev(bt mod P) + P k
@@ -488,15 +468,6 @@ struct PassArgs {
     // no scattered 16-B stores.
     uint32_t wil, wbrev;
 };
-
-// The line map is compiled only into the chunked-pair instances (NTS 2 / 3):
-// unchunked passes keep the plain index path (the run-time map cost ~1 % on
-// the C4 mode-2 passes, tools/ab.sh)
-template <int NTS>
-__device__ __forceinline__ uint64_t global_line(const PassArgs& a, uint64_t l) {
-    if constexpr (NTS == 2 || NTS == 3) return a.d0 + (l & a.wmask) + ((l & ~a.wmask) << a.log_sh);
-    else return l;
-}
 
 __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, uint32_t nblocks) {
     if (log_xg == 0 || (nblocks & ((8u << log_xg) - 1))) return b;
@@ -531,10 +502,6 @@ struct PassCfg {
     static constexpr int wpe = NT >= 256 ? (NT * PIFFT_MIN_WG_PER_CU) / 256 : 1;
     static constexpr int waves_per_eu = wpe > 4 ? 4 : wpe;
 };
-
-#ifndef PIFFT_REMAT16
-#define PIFFT_REMAT16 0  // 16-value exchanges: LDS addresses recomputed per component (tuning)
-#endif
 
 // LDS image of a workgroup's C lines during an exchange (one component, T
 // scalars): element r of line c sits at c*ls + swz(r), swz(r) = (r XOR ((r >>
@@ -739,11 +706,7 @@ constexpr int pre_count() {
 #ifndef PIFFT_SERIAL_BFLY
 #define PIFFT_SERIAL_BFLY 1
 #endif
-// PH (phase): 0 the whole pass for one tile; 1 only the first stage's loads
-// (and MODE 2's inter-pass twiddle fetch, into twp); 2 everything after them
-// (k_pass with H sub-tiles: every sub-tile's loads first, then one sub-tile
-// after the other)
-template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT, int PH = 0>
+template <typename T, int R, int C, int MODE, int NTS, int LP, int S, int VPT>
 __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v, cx<T>* pre, int tid, uint64_t tile,
                                             cx<T>* twp) {
     using C2 = cx<T>;
@@ -784,7 +747,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     // shared: fetched once, for u = 0.
     constexpr bool share_anc = St::cfast && U > 1 && St::NT % C == 0;
     [[maybe_unused]] C2* tw_pre = twp;  // 4 U entries (k_pass: first_tw_count)
-    if constexpr (St::first && BM == 2 && PH != 2) {
+    if constexpr (St::first && BM == 2) {
         const C2* tlo = static_cast<const C2*>(a.tw_lo);
         const C2* thi = static_cast<const C2*>(a.tw_hi);
         const uint64_t hmask = (1ull << a.tw_h) - 1;
@@ -792,7 +755,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int u = 0; u < U; u++) {
             int c, b;
             St::map(tid, u, c, b);
-            const uint64_t jm = (global_line<NTS>(a, (tile * C + c) & lb_mask) >> wil) & ns_mask;
+            const uint64_t jm = (((tile * C + c) & lb_mask) >> wil) & ns_mask;
             const uint64_t e0 = (jm * (uint64_t)NB) << a.tw_shift, e1 = (jm * (uint64_t)b) << a.tw_shift;
             if (!share_anc || u == 0) {
                 tw_pre[4 * u + 0] = tlo[e0 & hmask];
@@ -802,7 +765,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             tw_pre[4 * u + 3] = thi[e1 >> a.tw_h];
         }
     }
-    if constexpr (St::first && PH != 2) {
+    if constexpr (St::first) {
         // ---- inputs straight from HBM (all loads issued before any use) ----
         const C2* __restrict__ in = static_cast<const C2*>(a.in);
 #pragma unroll
@@ -814,15 +777,14 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             constexpr bool CL = clamp_loads<T>();
             const bool ok = CL || tile * C + c < a.nlines;
             const uint64_t line = (!CL || tile * C + c < a.nlines) ? tile * C + c : a.nlines - 1;
-            const uint64_t bt = line >> lbi, l = line & lb_mask;
-            constexpr bool CHUNK = NTS == 2 || NTS == 3;
-            const uint64_t j = (CHUNK && a.rd_virt) ? l : global_line<NTS>(a, l);
-            const uint32_t les = CHUNK ? a.in_log_es : lbi;
+            const uint64_t bt = line >> lbi, j = line & lb_mask;
+            const uint32_t les = lbi;
             // MODE 3: transform bt is worker (bt mod nq) of batch bt / nq, and
             // the leaves come from that batch's input
             const uint64_t bin = BM == 3 ? (bt >> a.log_nq) : bt;
             const C2* src = in + bin * a.in_bstride + j + ((uint64_t)b << les);
             if constexpr (BM == 3) {
+                static_assert(!WIL, "the fused tree pass is slice-major only");
                 // z_q[zi] from the P leaves x[zi + m M] (M = 2^(log_lb + LOGR)),
                 // G elements (G*P = 8 loads in flight) per round: no spills up
                 // to P = 8 at 128 VGPRs.  Small tiles (<= 256 threads: a
@@ -840,18 +802,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 constexpr int G = P >= TL ? 1 : TL / P;
                 static_assert(q % G == 0, "whole rounds of leaf loads");
                 const uint32_t log_m = log_lb + Sh::LOGR;
-                // MODE 11 (= 3 | 8, all workers, worker-interleaved layout):
-                // launch line l = (jw << wil) + wq is worker wq's line jw; its
-                // leaves sit at jw + r M/R + m M of the transform's input, and
-                // the lanes of one jw (c-fast) load the same leaves (one
-                // address per P lanes) while each evaluates its own worker's
-                // path
-                const uint64_t jw = WIL ? (j >> wil) : j;
-                const uint32_t wq = WIL ? (uint32_t)(j & ((1ull << wil) - 1))
-                                        : a.worker + (uint32_t)(tile * C >> log_lb & ((1u << a.log_nq) - 1));
-                const C2* lsrc = WIL ? in + bin * a.in_bstride + jw + ((uint64_t)b << log_lb) : src;
+                const uint32_t wq = a.worker + (uint32_t)(tile * C >> log_lb & ((1u << a.log_nq) - 1));
+                const C2* lsrc = src;
                 // this thread's base twiddles w_N^{zi0 2^t}, zi0 = its k = 0 input
-                const uint64_t zi0 = jw + ((uint64_t)b << log_lb);
+                const uint64_t zi0 = j + ((uint64_t)b << log_lb);
                 C2 bt[LP];
 #pragma unroll
                 for (int t = 0; t < LP; t++) bt[t] = tree_tw_lv<T>(a.tree, zi0, t);
@@ -872,7 +826,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     });
                     __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
                 });
-            } else if constexpr (BM == 2 && !CHUNK) {
+            } else if constexpr (BM == 2) {
                 // rows 2^les + in_pad apart (padded workspace, PassArgs::in_pad)
                 const uint64_t rs = (1ull << les) + a.in_pad;
                 const C2* row = in + bin * a.in_bstride + j + (uint64_t)b * rs;
@@ -886,7 +840,6 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             }
         }
     }
-    if constexpr (PH == 1) return;
     if constexpr (St::first && tw_prefetch<R, C, BM, VPT>()) {
         const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
         static_for<1, Sh::NSTG, 1>([&](auto sc) {
@@ -968,11 +921,9 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const uint64_t line = tile * C + c;
             if (line < a.nlines) {
-                const uint64_t bt = line >> lbi, l = line & lb_mask;
-                constexpr bool CHUNK = NTS == 2 || NTS == 3;
-                const uint64_t lj = (CHUNK && a.wr_virt) ? l : global_line<NTS>(a, l);
+                const uint64_t bt = line >> lbi, lj = line & lb_mask;
                 const uint64_t j = lj >> wil;  // the worker's own line
-                const uint32_t lns = CHUNK ? a.out_log_ns : (uint32_t)log_ns;
+                const uint32_t lns = (uint32_t)log_ns;
                 const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
                 if constexpr (WIL) {
                     // worker q at slot q (or bitrev(q): the natural-order result)
@@ -987,7 +938,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     const uint32_t il = a.ilv_log;
                     const uint64_t rq = il ? (uint64_t)(__builtin_bitreverse32((uint32_t)bt) >> (32 - il)) : 0;
                     // (out_pad: the line block's offset in a padded workspace)
-                    const uint64_t pad = CHUNK ? 0 : (j >> a.out_pad_log) * a.out_pad;
+                    const uint64_t pad = (j >> a.out_pad_log) * a.out_pad;
                     C2* dst = out + (bt >> il) * a.out_bstride + rq + (pos << il) + pad;
                     const uint32_t ks = lns + il;
 #pragma unroll
@@ -1029,10 +980,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         for (int comp = 0; comp < 2; comp++) {
             // (the tile's first LDS store has no earlier reader to wait for)
             if (S > 0 || comp > 0) lds_handoff<Nx::wave_private>();
-            // PIFFT_REMAT16: the second component's LDS addresses from an opaque
-            // tid copy (as the packed VPT-32 exchange does), not kept live
-            int tidc = tid;
-            if (PIFFT_REMAT16 && comp) asm volatile("" : "+v"(tidc));
+            const int tidc = tid;
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 int c, b;
@@ -1279,13 +1227,11 @@ constexpr int first_tw_count() {
 }
 
 // Workgroups per CU a k_pass instance is built for: two (PIFFT_MIN_WG_PER_CU),
-// one with H = 2 sub-tiles (the second sub-tile's data waits in registers:
-// two fp32 sub-tiles spill at 128 VGPRs)
-template <typename T, int R, int C, int MODE, int LP, int VPT, int H>
+// one for the fused tree pass at P = 16 (its 16 leaves per input)
+template <typename T, int R, int C, int MODE, int LP, int VPT>
 constexpr int pass_waves_per_eu() {
     constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
-    if constexpr (H > 1) return w > 2 ? w / 2 : w;
-    else return ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
+    return ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)
@@ -1295,13 +1241,8 @@ constexpr int pass_waves_per_eu() {
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
 // NTS: non-temporal streaming of the data (nt_loads / nt_stores)
-// H: sub-tiles per workgroup.  H = 2: the workgroup owns 2 C adjacent lines
-// and issues both halves' loads first (2 C-line row segments on a strided
-// read side, e.g. 256 B for fp64 C = 8), then runs one half's stages and
-// stores while the other half's data waits in registers, then the other half
-// (its stages overlap the first half's stores).  Same LDS as H = 1.
-template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16, int H = 1>
-__global__ __launch_bounds__((PassCfg<R, C, VPT>::NT), (pass_waves_per_eu<T, R, C, MODE, LP, VPT, H>()))
+template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16>
+__global__ __launch_bounds__((PassCfg<R, C, VPT>::NT), (pass_waves_per_eu<T, R, C, MODE, LP, VPT>()))
 void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     constexpr int Q = PassShape<R, VPT>::Q;
@@ -1314,13 +1255,12 @@ void k_pass(PassArgs a) {
     T* lds = reinterpret_cast<T*>(pifft_smem);
     const int tid = (int)threadIdx.x;
     if constexpr (VPT == 32 && std::is_same_v<T, float> && PIFFT_PACK32) {
-        static_assert(H == 1, "packed VPT-32: one tile per workgroup");
         cx<f2> vp[PassShape<R, VPT>::Q / 2];
         cx<float> twp[TWN];
         pass_stages_packed<R, C, MODE, NTS, 0>(a, reinterpret_cast<float*>(pifft_smem), vp, tid, tile, twp);
         (void)pre;
         (void)lds;
-    } else if constexpr (H == 1) {
+    } else {
         if (a.ilv_log && a.log_lb >= (uint32_t)ilog2c(C)) {
             // natural-order store: the P workers' tiles of one line block run
             // back to back (and on one XCD, log_xg >= log2 P), so the P 16-B
@@ -1332,22 +1272,6 @@ void k_pass(PassArgs a) {
         cx<T> v[Q];
         cx<T> twp[TWN];
         pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, lds, v, pre, tid, tile, twp);
-    } else {
-        cx<T> v[H][Q];
-        cx<T> twp[H][TWN];
-#pragma unroll
-        for (int h = 0; h < H; h++)
-            pass_stages<T, R, C, MODE, NTS, LP, 0, VPT, 1>(a, lds, v[h], pre, tid, tile * H + h, twp[h]);
-        // (scheduling barriers: the sub-tiles run one after the other -- the
-        // compiler would otherwise interleave their independent arithmetic and
-        // hold both sub-tiles' temporaries at once)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int h = 0; h < H; h++) {
-            if (h) __syncthreads();  // the previous sub-tile's last LDS reads are done
-            pass_stages<T, R, C, MODE, NTS, LP, 0, VPT, 2>(a, lds, v[h], pre, tid, tile * H + h, twp[h]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
     }
 }
 

@@ -11,12 +11,11 @@
 
 using namespace pifft;
 
-#define PKVH(T, PREC, R, C, MODE, NTS, LP, VPT, H)                                                          \
-    PassKernel {                                                                                             \
-        PREC, R, C, MODE, NTS, LP, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS, LP, VPT, H>), \
-            PassCfg<R, C, VPT>::NT, pass_lds_bytes<T, R, C, MODE, VPT>(), VPT, H                           \
+#define PKV(T, PREC, R, C, MODE, NTS, LP, VPT)                                                          \
+    PassKernel {                                                                                        \
+        PREC, R, C, MODE, NTS, LP, reinterpret_cast<const void*>(&k_pass<T, R, C, MODE, NTS, LP, VPT>), \
+            PassCfg<R, C, VPT>::NT, pass_lds_bytes<T, R, C, MODE, VPT>(), VPT                           \
     }
-#define PKV(T, PREC, R, C, MODE, NTS, LP, VPT) PKVH(T, PREC, R, C, MODE, NTS, LP, VPT, 1)
 #define PK(T, PREC, R, C, MODE, NTS, LP) PKV(T, PREC, R, C, MODE, NTS, LP, 16)
 
 namespace {

@@ -9,8 +9,7 @@ struct PassKernel {
     const void* fn;
     int nt;
     int lds_bytes;
-    int vpt;  // values per thread (16, or 8 for small single-pass launches)
-    int h;    // sub-tiles per workgroup (k_pass H)
+    int vpt;  // values per thread (16; 32 for the packed fp32 passes)
 };
 
 }  // namespace pifft

@@ -22,7 +22,7 @@ F32, F64 = 32, 64
 OUT_NATURAL, OUT_SLICES, OUT_BITREV = 0, 1, 2
 PROFILE_ALL, PROFILE_SAMPLED = 0, 1
 SEPARATE_TREE = 4  # flag bit: the tree never fused into the first pass (CLI -u)
-KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass", 5: "chunk-a", 6: "chunk-b"}
+KIND_NAMES = {1: "tree", 2: "pass", 3: "interleave", 4: "tree+pass"}
 MAX_LAUNCH_INFO = 256  # PIFFT_MAX_LAUNCH_INFO (include/pifft.h)
 
 
@@ -49,7 +49,6 @@ class PlanInfo(ctypes.Structure):
         ("tree_launches", ctypes.c_int32),
         ("radix", ctypes.c_int32 * 8),
         ("lines", ctypes.c_int32 * 8),
-        ("chunk_pairs", ctypes.c_int32),
         ("launch_bytes", ctypes.c_uint64 * MAX_LAUNCH_INFO),
         ("launch_kind", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("launch_fn", ctypes.c_int32 * MAX_LAUNCH_INFO),
@@ -252,7 +251,6 @@ def describe_info(i: PlanInfo) -> dict:
         "radix": list(i.radix[: i.num_passes]), "lines": list(i.lines[: i.num_passes]),
         "launch_bytes": list(i.launch_bytes[: min(nl, MAX_LAUNCH_INFO)]),
         "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, MAX_LAUNCH_INFO)]],
-        "chunk_pairs": i.chunk_pairs,
         "launch_fn": list(i.launch_fn[: min(nl, MAX_LAUNCH_INFO)]),
         "vpt": list(i.vpt[: i.num_passes]),
         "worker_interleaved": bool(i.layout & 1), "natural_store": bool(i.layout & 2),

@@ -27,6 +27,10 @@
  * (the reference's segment q of its bit-reversed scratch).  A plan computes a
  * contiguous range of workers [first, first+count) on one GPU; a plan with
  * count == P on one GPU is the whole transform.
+ *
+ * Plans depend only on the arguments: the planner's PIFFT_* tuning variables
+ * (used by the repository's measurement tools) are read only when
+ * PIFFT_TUNING=1 is set in the environment.
  */
 #ifndef PIFFT_H
 #define PIFFT_H
@@ -85,17 +89,15 @@ typedef struct pifft_plan_info {
     int32_t tree_launches;   /* launches of the tree ("funnel") stage              */
     int32_t radix[8];        /* LDS-resident sub-FFT length of each pass           */
     int32_t lines[8];        /* columns per workgroup of each pass                 */
-    int32_t chunk_pairs;     /* chunked last-two-pass pairs (2 launches each; 0 = none) */
     uint64_t launch_bytes[PIFFT_MAX_LAUNCH_INFO]; /* algorithmic bytes of each launch
                                   (read+write of the data, twiddle tables excluded) */
     int32_t launch_kind[PIFFT_MAX_LAUNCH_INFO]; /* 1 tree, 2 pass, 3 interleave, 4 tree fused
-                                  into a pass, 5 / 6 first / second half of a chunked
-                                  pass pair (intermediate in the Infinity Cache) */
+                                  into a pass */
     int32_t launch_fn[PIFFT_MAX_LAUNCH_INFO]; /* kernel of each launch: launches with the same id
                                   run the same kernel function (ids 0, 1, ... in order
                                   of first use) -- what rocprof aggregates per kernel */
-    int32_t vpt[8];          /* complex values per thread of each pass (16; 8 for single
-                                passes too small to fill the GPU at 16)            */
+    int32_t vpt[8];          /* complex values per thread of each pass (16; 32 for the
+                                packed fp32 passes of large transforms)            */
     int32_t layout;          /* bit 0: worker-interleaved passes (all P <= 16 workers of a
                                 natural-order plan: the last pass writes natural order);
                                 bit 1: the last pass stores natural order from the

@@ -231,37 +231,6 @@ ORDERS = {"0": [1024, 512, 512], "1": [512, 512, 1024]}  # PIFFT_POS_MODEL: the 
 
 
 @pytest.mark.parametrize("pos", ["0", "1"])
-@pytest.mark.parametrize("prec,passes", [(pifft.F64, "0"), (pifft.F32, "3")])
-def test_subtiled_passes_bitwise_equal(prec, passes, pos, monkeypatch):
-    """k_pass with two sub-tiles per workgroup (H = 2, PIFFT_SUBTILES) runs the
-    same per-line arithmetic as H = 1: the 2^28 plan's output is bitwise
-    equal (fp64, fp32 forced to three passes; both radix orders)."""
-    n = 1 << 28
-    monkeypatch.setenv("PIFFT_POS_MODEL", pos)
-    cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
-    st = torch.cuda.current_stream()
-    x = torch.empty(n, dtype=cdt, device="cuda")
-    pifft.generate_device(x.data_ptr(), n, n, prec, seed=21, stream=st)
-    if passes != "0":
-        monkeypatch.setenv("PIFFT_PASSES", passes)
-        monkeypatch.setenv("PIFFT_VPT32", "0")  # sub-tiles are a 16-value form
-    base = pifft.Plan(n, 1, 1, prec)
-    monkeypatch.setenv("PIFFT_SUBTILES", "2")
-    sub = pifft.Plan(n, 1, 1, prec)
-    assert base.describe()["radix"] == sub.describe()["radix"]
-    if prec == pifft.F64:  # (the fp32 8192-value tile's 1024-point pass has 64-B segments: no position model)
-        assert base.describe()["radix"] == ORDERS[pos]
-    assert [2 * c for c in base.describe()["lines"]] == sub.describe()["lines"]
-    ya = torch.empty_like(x)
-    base.execute_device(x.data_ptr(), ya.data_ptr(), st)
-    base.close()
-    yb = torch.empty_like(x)
-    sub.execute_device(x.data_ptr(), yb.data_ptr(), st)
-    torch.cuda.synchronize()
-    assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb))
-
-
-@pytest.mark.parametrize("pos", ["0", "1"])
 def test_packed_vpt32_fp32_three_pass_bitwise(pos, monkeypatch):
     """fp32 2^28 in three passes on the 16384-value tile: the packed VPT-32
     passes (512 threads, two butterflies per register pair, PIFFT_VPT32=1)

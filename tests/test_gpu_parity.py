@@ -674,66 +674,6 @@ def test_bitrev_host_boundary_segments():
     assert_bins_close(out[2 * m:], want[2 * m:], "f64", n)
 
 
-# --------------------------------------------------- chunked pass pairs ---
-def _plan_env(monkeypatch, env, *a, **k):
-    for key, v in env.items():
-        monkeypatch.setenv(key, str(v))
-    try:
-        return pifft.Plan(*a, **k)
-    finally:
-        for key in env:
-            monkeypatch.delenv(key)
-
-
-@pytest.mark.parametrize("suf,logn,P,batch,env", [
-    ("f64", 22, 1, 1, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 16}),   # 4 residue chunks
-    ("f64", 21, 1, 4, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 64}),   # groups of 2 whole transforms
-    ("f32", 24, 1, 1, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 16}),   # 8 residue chunks
-    ("f64", 24, 4, 1, {"PIFFT_NT": 1, "PIFFT_CHUNK_MIB": 16}),   # fused tree + chunked pair
-    ("f64", 24, 1, 1, {"PIFFT_CHUNK_MIB": 128}),                 # 2 chunks at the natural NT threshold
-])
-def test_chunked_pass_pair(suf, logn, P, batch, env, monkeypatch):
-    """The last two passes run chunk by chunk through an Infinity-Cache-sized
-    scratch: same arithmetic per element, so the result must equal the
-    unchunked plan bit for bit, and the oracle within tolerance."""
-    n = 1 << logn
-    q = P - 1
-    kw = dict(first=q, count=1, device=0, flags=pifft.OUT_SLICES) if P > 1 else {}
-    chunked = _plan_env(monkeypatch, env, n, P, batch, PREC[suf], **kw)
-    d = chunked.describe()
-    assert d["chunk_pairs"] >= 2 and "chunk-a" in d["launch_kind"] and "chunk-b" in d["launch_kind"]
-    plain = _plan_env(monkeypatch, dict(env, PIFFT_CHUNK_MIB=0), n, P, batch, PREC[suf], **kw)
-    assert plain.describe()["chunk_pairs"] == 0
-    x = np.concatenate([oracle.generate(n, DT[suf], seed=logn + b) for b in range(batch)])
-    got = run(chunked, x)
-    assert np.array_equal(got.view(np.uint8), run(plain, x).view(np.uint8))
-    if logn <= 22:
-        for b in range(batch):
-            want = oracle.fft(x[b * n:(b + 1) * n], P=8, nthreads=8)
-            if P > 1:
-                want = pifft_dist.slice_of_natural(want, P, q)
-            m = n // P
-            assert_bins_close(got[b * m:(b + 1) * m], want, suf, n)
-
-
-def test_chunked_pass_pair_config4_bitwise(monkeypatch):
-    """Config 4 (fp64 2^28, one GPU): the chunked plan equals the unchunked one
-    bit for bit (the property tests above check it against the DFT)."""
-    n = 1 << 28
-    x = torch.empty(n, dtype=torch.complex128, device="cuda")
-    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=torch.cuda.current_stream())
-    chunked = _plan_env(monkeypatch, {"PIFFT_CHUNK_MIB": 128}, n, 1, 1, pifft.F64)
-    assert chunked.describe()["chunk_pairs"] > 0
-    a = torch.empty_like(x)
-    chunked.execute_device(x.data_ptr(), a.data_ptr(), torch.cuda.current_stream())
-    del chunked
-    plain = _plan_env(monkeypatch, {"PIFFT_CHUNK_MIB": 0}, n, 1, 1, pifft.F64)
-    b = torch.empty_like(x)
-    plain.execute_device(x.data_ptr(), b.data_ptr(), torch.cuda.current_stream())
-    torch.cuda.synchronize()
-    assert torch.equal(torch.view_as_real(a), torch.view_as_real(b))
-
-
 # ---------------------------------------- worker-interleaved layout (wil) ---
 @pytest.mark.parametrize("suf,logn,P,batch", [("f64", 20, 8, 1), ("f64", 21, 2, 2), ("f32", 20, 8, 3),
                                               ("f64", 19, 16, 1), ("f32", 22, 4, 1), ("f64", 18, 8, 2),
@@ -763,41 +703,6 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
     for bt in range(batch):
         assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
 
-
-@pytest.mark.parametrize("suf,logn,P,batch,cf", [("f64", 20, 8, 1, 0), ("f32", 20, 8, 3, 0), ("f64", 20, 16, 1, 0),
-                                                 ("f64", 22, 4, 1, 0), ("f64", 21, 8, 2, 16), ("f32", 23, 16, 1, 8),
-                                                 ("f64", 19, 8, 1, 32), ("f32", 18, 4, 2, 32)])
-def test_worker_interleaved_fused_tree_vs_oracle(suf, logn, P, batch, cf, monkeypatch):
-    """The tree fused into the first worker-interleaved pass (MODE 11,
-    PIFFT_WIL_FUSE=1; PIFFT_WIL_FUSE_C lines per workgroup): no tree launch,
-    each lane evaluating its own worker's path from leaves shared by the P
-    lanes of its line block.  Within tolerance of the oracle and of the
-    unfused plan (the fused path uses factored tree twiddles: not bitwise)."""
-    n = 1 << logn
-    x = oracle.generate(n * batch, DT[suf], seed=logn * 5 + P)
-    d_in = dev(x)
-    st = torch.cuda.current_stream()
-    monkeypatch.setenv("PIFFT_WIL_FUSE", "1")
-    if cf:
-        monkeypatch.setenv("PIFFT_WIL_FUSE_C", str(cf))
-    fused = pifft.Plan(n, P, batch, PREC[suf])
-    d = fused.describe()
-    assert d["worker_interleaved"] and d["launch_kind"][0] == "tree+pass" and "tree" not in d["launch_kind"], d
-    if cf:
-        assert d["lines"][0] == cf
-    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")
-    plain = pifft.Plan(n, P, batch, PREC[suf])
-    assert plain.describe()["launch_kind"][0] == "tree"
-    a = torch.empty_like(d_in)
-    b = torch.empty_like(d_in)
-    fused.execute_device(d_in.data_ptr(), a.data_ptr(), st)
-    plain.execute_device(d_in.data_ptr(), b.data_ptr(), st)
-    torch.cuda.synchronize()
-    got, ref = a.cpu().numpy().reshape(batch, n), b.cpu().numpy().reshape(batch, n)
-    for bt in range(batch):
-        want = oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8)
-        assert_bins_close(got[bt], want, suf, n)
-        assert_bins_close(got[bt], ref[bt], suf, n)
 
 
 # ------------------------------------------------ the final exchange (8e) ---
@@ -985,29 +890,6 @@ def test_sweep_drives_the_mi355x_cli(tmp_path):
     lines = txt.splitlines()
     assert lines[0].startswith("Empirical time complexity of pi-DFT on NVIDIA GPU (p=8, 2 replications)")
     assert [int(ln.split()[0]) for ln in lines[3:]] == [1 << e for e in range(16, 21)]
-
-
-@pytest.mark.parametrize("suf,logn,P,batch", [("f64", 20, 4, 1), ("f64", 22, 8, 1), ("f32", 20, 8, 1), ("f64", 24, 2, 1), ("f64", 18, 2, 3)])
-def test_fused_tree_all_workers(suf, logn, P, batch, monkeypatch):
-    """The tree fused into the first pass of a plan holding ALL P workers
-    (off by default, PIFFT_FUSE_ALL_MAX_MIB): the worker of each tile comes
-    from its transform index (PassArgs.log_nq).  Same result as the unfused
-    plan and the oracle."""
-    n = 1 << logn
-    x = oracle.generate(n * batch, DT[suf], seed=logn + P)
-    monkeypatch.setenv("PIFFT_FUSE_ALL_MAX_MIB", "100000")
-    monkeypatch.setenv("PIFFT_WORKER_IL", "0")  # (the worker-interleaved layout takes precedence)
-    fused = pifft.Plan(n, P, batch, PREC[suf])
-    monkeypatch.delenv("PIFFT_FUSE_ALL_MAX_MIB")
-    plain = pifft.Plan(n, P, batch, PREC[suf])
-    kinds = fused.describe()["launch_kind"]
-    if "tree+pass" not in kinds:
-        pytest.fail(f"no fused instance for this plan: {fused.describe()['radix']} {fused.describe()['lines']} {kinds}")
-    assert plain.describe()["launch_kind"][0] == "tree"
-    got = run(fused, x).reshape(batch, n)
-    assert rel_l2(got.reshape(-1), run(plain, x)) <= tol(suf, n)
-    for bt in range(batch):
-        assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
 
 
 def test_concurrent_plans_from_host_threads():

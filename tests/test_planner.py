@@ -58,40 +58,7 @@ def test_config4_2e28_fp64():
     assert d["radix"] == [512, 512, 1024] and d["lines"] == [16, 16, 8]
     assert pifft.dry_run(1 << 29, 1, 1, F64)["radix"] == [512, 1024, 1024]
     assert d["launch_bytes"] == [2 * (1 << 28) * 16] * 3
-    assert d["workspace_bytes"] >= 4 * GiB and d["chunk_pairs"] == 0
-
-
-def test_config4_chunked_pairs(monkeypatch):
-    """PIFFT_CHUNK_MIB=128: pass 1 through HBM, passes 2+3 as chunked pairs
-    through a 128 MiB (Infinity-Cache sized) scratch: 32 chunks of 32
-    residues, 2 launches each, same algorithmic bytes."""
-    monkeypatch.setenv("PIFFT_CHUNK_MIB", "128")
-    d = pifft.dry_run(1 << 28, 1, 1, F64)
-    assert d["launch_kind"] == ["pass"] + ["chunk-a", "chunk-b"] * 32 and d["chunk_pairs"] == 32
-    assert d["launch_bytes"][0] == 2 * (1 << 28) * 16
-    assert d["launch_bytes"][1:] == [2 * (128 << 20)] * 64
-    assert sum(d["launch_bytes"]) == 3 * 2 * (1 << 28) * 16
-    assert d["workspace_bytes"] >= 4 * GiB + (128 << 20)
-
-
-def test_chunked_pair_rules(monkeypatch):
-    """Chunking (PIFFT_CHUNK_MIB > 0) applies to the last two passes of
-    >= 3-pass plans whose passes stream more than the Infinity Cache."""
-    monkeypatch.setenv("PIFFT_CHUNK_MIB", "128")
-    d = pifft.dry_run(1 << 24, 1, 1, F64)  # 256 MiB each side
-    assert d["chunk_pairs"] == 2 and d["launch_kind"] == ["pass"] + ["chunk-a", "chunk-b"] * 2
-    assert pifft.dry_run(1 << 20, 1, 1, F64)["chunk_pairs"] == 0      # two passes
-    assert pifft.dry_run(1 << 22, 1, 1, F64)["chunk_pairs"] == 0      # cache-resident
-    assert pifft.dry_run(4096, 1, 4096, F32)["chunk_pairs"] == 0      # single pass
-    # bit-reversed output keeps its MODE 6 last pass
-    assert pifft.dry_run(1 << 28, 1, 1, F64, flags=pifft.OUT_BITREV)["chunk_pairs"] == 0
-    # batched transforms that each fit the scratch: groups of whole transforms
-    monkeypatch.setenv("PIFFT_NT", "1")
-    monkeypatch.setenv("PIFFT_CHUNK_MIB", "64")
-    d = pifft.dry_run(1 << 21, 1, 4, F64)
-    assert d["chunk_pairs"] == 2 and d["launch_bytes"][1:] == [2 * (64 << 20)] * 4
-    monkeypatch.setenv("PIFFT_CHUNK_MIB", "0")
-    assert pifft.dry_run(1 << 28, 1, 1, F64)["chunk_pairs"] == 0
+    assert d["workspace_bytes"] >= 4 * GiB
 
 
 @pytest.mark.parametrize("P", [2, 4, 8, 16])
@@ -257,3 +224,29 @@ def test_position_model_not_for_worker_interleaved_plans():
     assert wil["worker_interleaved"] and wil["radix"] == [1024, 512, 512]
     assert pifft.dry_run(1 << 28, 1, 1, F64)["radix"] == [512, 512, 1024]
     assert pifft.dry_run(1 << 27, 2, 1, F32)["radix"] == [512, 512, 256]
+
+
+STRAY = {"PIFFT_ORDER": "1", "PIFFT_PASSES": "4", "PIFFT_RADIX_LOGS": "10,10,8", "PIFFT_NT": "0",
+         "PIFFT_WORKER_IL": "0", "PIFFT_POS_MODEL": "0", "PIFFT_VPT32": "0", "PIFFT_W_PAD": "0",
+         "PIFFT_TILE64": "4096", "PIFFT_LAST_C": "16", "PIFFT_FUSE_TREE": "0", "PIFFT_ILV": "1",
+         "PIFFT_SINGLE_TILE32": "8192"}
+
+
+@pytest.mark.parametrize("shape", [(1 << 28, 1, 1, F64, 0, 1, 0), (1 << 28, 1, 1, F32, 0, 1, 0),
+                                   (1 << 20, 8, 1, F64, 0, 8, 0), (1 << 20, 8, 1, F64, 0, 1, 1),
+                                   (4096, 1, 4096, F32, 0, 1, 0), (1 << 32, 8, 1, F64, 7, 1, 1)])
+def test_stray_tuning_variables_are_ignored(shape, monkeypatch):
+    """Without PIFFT_TUNING=1 the planner reads none of its tuning variables:
+    a stray PIFFT_ORDER / PIFFT_PASSES / ... inherited from a shell leaves the
+    product's plan unchanged (round-3 verdict, knob debt)."""
+    n, P, b, prec, first, count, flags = shape
+    monkeypatch.delenv("PIFFT_TUNING")
+    want = pifft.dry_run(n, P, b, prec, first=first, count=count, flags=flags)
+    for k, v in STRAY.items():
+        monkeypatch.setenv(k, v)
+    assert pifft.dry_run(n, P, b, prec, first=first, count=count, flags=flags) == want
+    monkeypatch.setenv("PIFFT_TUNING", "0")
+    assert pifft.dry_run(n, P, b, prec, first=first, count=count, flags=flags) == want
+    # ... and the same variables do take effect under PIFFT_TUNING=1
+    monkeypatch.setenv("PIFFT_TUNING", "1")
+    assert pifft.dry_run(n, P, b, prec, first=first, count=count, flags=flags) != want

@@ -38,11 +38,11 @@ def main():
             for _ in range(2):
                 plan.execute_device(x.data_ptr(), y.data_ptr(), s)
             torch.cuda.synchronize()
-            plan.profile_start(STEPS)
+            plan.profile_start(STEPS, pifft.PROFILE_ALL)  # every launch of every execution
             for _ in range(STEPS):
                 plan.execute_device(x.data_ptr(), y.data_ptr(), s)
-            used, sums = plan.profile_read()
-            ms = [v / used for v in sums]
+            used, sums, cnt = plan.profile_read()
+            ms = [v / c for v, c in zip(sums, cnt)]
             if best is None or sum(ms) < sum(best):
                 best = ms
         va = y.data_ptr()

@@ -15,6 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
+os.environ["PIFFT_TUNING"] = "1"  # libpifft reads the variants' PIFFT_* variables only then
 
 
 def main():
