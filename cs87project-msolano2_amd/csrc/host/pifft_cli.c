@@ -14,7 +14,9 @@
  *         [-w file] [-r] [-u] [-x] [-W warmups] [-l]
  *
  * Output: the reference's 5-column TSV "n p total stage1 stage2" in ms
- * (CPU.c:485-492), once.  stage 1 = tree, stage 2 = local FFT (+ reorder).
+ * (CPU.c:485-492), once.  stage 1 = tree, stage 2 = local FFT (+ reorder),
+ * each the device wall time from before its first launch to after its last
+ * (the reference's tm_funnel / tm_tube wall-clock timers, CPU.c:414-481).
  * With several GPUs the time is the slowest GPU's (the reference prints worker
  * 0's own timers without a barrier; here all GPUs are waited for).
  * Extensions: -f precision (default 32 = the reference's data_t), -b batch of
@@ -24,7 +26,9 @@
  * scratch order (bit-reversed, tmp_in before CPU.c:496-499's scatter; no
  * reorder launch), -u keep the tree its own launch (never fused into the first
  * pass: stage 1 = the tree alone, as the reference's funnel timer, for the
- * cost-law fit of analyze-results.R:56), -x extra columns (GFLOP/s, GB/s),
+ * cost-law fit of analyze-results.R:56), -x extra columns (GFLOP/s, GB/s over
+ * the wall total, then the kernel-only stage sums: stage times without the
+ * gaps between launches),
  * -W untimed warm-up runs before the timed one (default 1; code-object load),
  * -l list GPUs (the how-many-* utilities).  -n is parsed as 64-bit.
  */
@@ -77,7 +81,7 @@ static void show_usage(void) {
               "  -w <file>  write the output (binary data_t; natural order unless -r)\n"
               "  -r         output in the reference's bit-reversed scratch order\n"
               "  -u         tree stage as its own launch (stage 1 = the tree alone)\n"
-              "  -x         extra columns: GFLOP/s, algorithmic GB/s\n"
+              "  -x         extra columns: GFLOP/s, algorithmic GB/s, kernel-only stage 1 / 2 ms\n"
               "  -W <w>     untimed warm-up runs (default 1)\n"
               "  -l         list GPUs and exit\n"
               "\n");
@@ -351,7 +355,7 @@ int run(tr_t* t) {
     }
     if (!t->test_mode) {
         if (!t->no_header) print_out("n\tp\ttime (total)\ttime (stage 1)\ttime (stage 2)%s\n",
-                                     t->extra ? "\tGFLOP/s\tGB/s" : "");
+                                     t->extra ? "\tGFLOP/s\tGB/s\tkernels (stage 1)\tkernels (stage 2)" : "");
         if (t->extra) {
             pifft_plan_info info;
             uint64_t bytes = 0;
@@ -361,8 +365,13 @@ int run(tr_t* t) {
             }
             const double ms = s1 + s2;
             const double flops = 5.0 * (double)t->N * log2((double)t->N) * t->batch;
-            print_out("%llu\t%u\t%lf\t%lf\t%lf\t%lf\t%lf\n", (unsigned long long)t->N, t->P, ms, s1, s2,
-                      flops / (ms * 1e6), (double)bytes / G / (ms * 1e6));
+            double k1 = 0, k2 = 0;
+            if (pifft_execute_group_kernel_times(plans, (int)G, &k1, &k2)) {
+                stderr_out("%s\n", pifft_last_error());
+                goto done;
+            }
+            print_out("%llu\t%u\t%lf\t%lf\t%lf\t%lf\t%lf\t%lf\t%lf\n", (unsigned long long)t->N, t->P, ms, s1, s2,
+                      flops / (ms * 1e6), (double)bytes / G / (ms * 1e6), k1, k2);
         } else {
             print_out("%llu\t%u\t%lf\t%lf\t%lf\n", (unsigned long long)t->N, t->P, s1 + s2, s1, s2);
         }

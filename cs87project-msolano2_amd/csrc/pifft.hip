@@ -179,6 +179,7 @@ struct pifft_plan {
     size_t tw_bytes = 0;
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;  // 2 per launch: its start and stop (launch_steps)
+    hipEvent_t sev[3] = {nullptr, nullptr, nullptr};  // stage markers: start, end of stage 1, end of stage 2
     void* d_hin = nullptr;   // pifft_execute's staging copies
     void* d_hout = nullptr;
     void* d_gather = nullptr;  // pifft_allgather: every worker's slices on this plan's device
@@ -545,6 +546,8 @@ void release(pifft_plan* p) {
     for (auto e : p->gev)
         if (e) (void)hipEventDestroy(e);
     for (auto e : p->ev) (void)hipEventDestroy(e);
+    for (auto e : p->sev)
+        if (e) (void)hipEventDestroy(e);
     for (auto e : p->prof_ev) (void)hipEventDestroy(e);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
@@ -887,6 +890,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     HIPCHK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->ev.resize(2 * p->steps.size());
     for (auto& e : p->ev) HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
+    for (auto& e : p->sev) HIPCHK(hipEventCreateWithFlags(&e, kTimingEventFlags));
     return 0;
 }
 
@@ -1022,12 +1026,39 @@ int run_timed(pifft_plan* p, const void* d_in, void* d_out, hipStream_t st, std:
     return read_launch_ms(p->steps.size(), p->ev.data(), ms);
 }
 
+bool stage1_step(const Step& s) { return s.kind == STEP_TREE || s.kind == STEP_TREE_PASS; }
+
 void stage_split(const pifft_plan* p, const std::vector<float>& ms, double* s1, double* s2) {
     double a = 0, b = 0;
-    for (size_t i = 0; i < ms.size(); i++)
-        (p->steps[i].kind == STEP_TREE || p->steps[i].kind == STEP_TREE_PASS ? a : b) += ms[i];
+    for (size_t i = 0; i < ms.size(); i++) (stage1_step(p->steps[i]) ? a : b) += ms[i];
     if (s1) *s1 = a;
     if (s2) *s2 = b;
+}
+
+// One execution timed like the reference's two stage timers (tm_funnel,
+// tm_tube: wall clock around each whole stage, CPU.c:414-481): a marker
+// event before the stage's first launch and after its last, so the gaps and
+// launch latency between kernels count.  (The stage-1 launches -- the tree,
+// or the tree fused into the first pass -- lead every plan.)
+int launch_stage_marked(pifft_plan* p, const void* d_in, void* d_out) {
+    HIPCHK(hipEventRecord(p->sev[0], p->stream));
+    size_t i = 0;
+    for (; i < p->steps.size() && stage1_step(p->steps[i]); i++)
+        if (launch_step(p, p->steps[i], d_in, d_out, p->stream)) return -1;
+    HIPCHK(hipEventRecord(p->sev[1], p->stream));
+    for (; i < p->steps.size(); i++)
+        if (launch_step(p, p->steps[i], d_in, d_out, p->stream)) return -1;
+    HIPCHK(hipEventRecord(p->sev[2], p->stream));
+    return 0;
+}
+int read_stage_marked(pifft_plan* p, double* s1, double* s2) {
+    float a = 0.0f, b = 0.0f;
+    HIPCHK(hipEventSynchronize(p->sev[2]));
+    HIPCHK(hipEventElapsedTime(&a, p->sev[0], p->sev[1]));
+    HIPCHK(hipEventElapsedTime(&b, p->sev[1], p->sev[2]));
+    *s1 = a;
+    *s2 = b;
+    return 0;
 }
 
 // device result of a plan holding only some workers (slice-major) -> their
@@ -1354,6 +1385,15 @@ int pifft_plan_tune_workspace(pifft_plan* p, const void* d_in, void* d_out, void
     for (int t = 1; t < tries && rc == 0; t++) {
         void* keep = p->buf[BUF_W];
         void* fresh = nullptr;
+        // the losers stay allocated until the end: try only while the device
+        // keeps room for another workspace and 4 GiB beyond this one (other
+        // processes on the GPU, e.g. bench.py's same-device rehearsal ranks,
+        // allocate concurrently)
+        size_t mfree = 0, mtotal = 0;
+        if (hipMemGetInfo(&mfree, &mtotal) != hipSuccess || mfree < 2 * p->bytes_w + (4ull << 30)) {
+            (void)hipGetLastError();
+            break;
+        }
         if (hipMalloc(&fresh, p->bytes_w) != hipSuccess) {
             (void)hipGetLastError();
             break;  // no room for another workspace: keep the best so far
@@ -1434,6 +1474,9 @@ int pifft_execute_device_timed(pifft_plan* p, const void* d_in, void* d_out, voi
     hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
     std::vector<float> ms;
     if (run_timed(p, d_in, d_out, st, ms)) return -1;
+    // (fence-free timing events: the output is complete and visible once the
+    // stream itself has drained)
+    HIPCHK(hipStreamSynchronize(st));
     if (launch_ms)
         for (int i = 0; i < max_launches && i < (int)ms.size(); i++) launch_ms[i] = ms[i];
     return 0;
@@ -1477,20 +1520,21 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
         DeviceGuard g(plans[i]->device);
         HIPCHK(hipStreamSynchronize(plans[i]->stream));
     }
-    // launch all GPUs, then wait for all
+    // launch all GPUs, then wait for all (stage markers: wall time per stage)
     for (int i = 0; i < np; i++) {
         pifft_plan* p = plans[i];
         DeviceGuard g(p->device);
-        if (launch_steps(p, p->d_hin, p->d_hout, p->stream, p->ev.data())) return -1;
+        if (launch_stage_marked(p, p->d_hin, p->d_hout)) return -1;
     }
     double t1 = 0, t2 = 0;
     for (int i = 0; i < np; i++) {
         pifft_plan* p = plans[i];
         DeviceGuard g(p->device);
-        std::vector<float> ms;
-        if (read_launch_ms(p->steps.size(), p->ev.data(), ms)) return -1;
         double a, b;
-        stage_split(p, ms, &a, &b);
+        if (read_stage_marked(p, &a, &b)) return -1;
+        // the timing events skip the system-scope fence: the stream itself is
+        // waited for before anything reads the result on the host
+        HIPCHK(hipStreamSynchronize(p->stream));
         if (a + b > t1 + t2) {  // the slowest GPU sets the job's time
             t1 = a;
             t2 = b;
@@ -1538,6 +1582,36 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
             scatter_to_host(p, p->host_tmp.data(), (char*)host_out);
         }
     }
+    return 0;
+}
+
+int pifft_execute_group_kernel_times(pifft_plan** plans, int np, double* ms1, double* ms2) {
+    if (!plans || np <= 0) return fail("no plans");
+    for (int i = 0; i < np; i++) {
+        if (!plans[i]) return fail("plan %d is NULL", i);
+        if (!plans[i]->d_hin || !plans[i]->d_hout) return fail("plan %d: no staged input (call pifft_execute_group first)", i);
+    }
+    for (int i = 0; i < np; i++) {
+        pifft_plan* p = plans[i];
+        DeviceGuard g(p->device);
+        if (launch_steps(p, p->d_hin, p->d_hout, p->stream, p->ev.data())) return -1;
+    }
+    double t1 = 0, t2 = 0;
+    for (int i = 0; i < np; i++) {
+        pifft_plan* p = plans[i];
+        DeviceGuard g(p->device);
+        std::vector<float> ms;
+        if (read_launch_ms(p->steps.size(), p->ev.data(), ms)) return -1;
+        HIPCHK(hipStreamSynchronize(p->stream));
+        double a, b;
+        stage_split(p, ms, &a, &b);
+        if (a + b > t1 + t2) {
+            t1 = a;
+            t2 = b;
+        }
+    }
+    if (ms1) *ms1 = t1;
+    if (ms2) *ms2 = t2;
     return 0;
 }
 

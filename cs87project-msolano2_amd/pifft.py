@@ -77,6 +77,9 @@ _SIGS = {
                                                   ctypes.c_int]),
     "pifft_execute": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]),
+    "pifft_execute_group_kernel_times": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int,
+                                                        ctypes.POINTER(ctypes.c_double),
+                                                        ctypes.POINTER(ctypes.c_double)]),
     "pifft_execute_group": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _P,
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "pifft_generate_device": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -309,6 +312,16 @@ def execute_group(plans, host_in, host_out=None):
     t1, t2 = ctypes.c_double(), ctypes.c_double()
     _check(lib().pifft_execute_group(arr, len(plans), host_in.ctypes.data, out_ptr, ctypes.byref(t1),
                                      ctypes.byref(t2)), "pifft_execute_group")
+    return t1.value, t2.value
+
+
+def execute_group_kernel_times(plans):
+    """pifft_execute_group_kernel_times: the kernel-only stage sums (ms) of the
+    slowest plan, re-running the last execute_group's staged input."""
+    arr = (_P * len(plans))(*[p.handle.value for p in plans])
+    t1, t2 = ctypes.c_double(), ctypes.c_double()
+    _check(lib().pifft_execute_group_kernel_times(arr, len(plans), ctypes.byref(t1), ctypes.byref(t2)),
+           "pifft_execute_group_kernel_times")
     return t1.value, t2.value
 
 

@@ -94,6 +94,60 @@ def slices_transform_major(gathered, world: int, batch: int):
     return gathered.reshape(world, batch, -1).transpose(0, 1).contiguous().reshape(-1)
 
 
+MASK64 = (1 << 64) - 1
+
+
+def tensor_digest(t, chunk: int = 1 << 24) -> tuple[int, int]:
+    """Two 64-bit digests of a tensor's BYTES (complex values as their integer
+    words): a position-weighted sum and a mixed sum, both mod 2^64.  Integer
+    sums are exact and order-independent, so equal bits give equal digests on
+    any device (bench.py's cross-rank bitwise check of the worker slices)."""
+    import torch
+    v = torch.view_as_real(t).reshape(-1) if t.is_complex() else t.reshape(-1)
+    v = v.view(torch.int64) if v.element_size() == 8 else v.view(torch.int32).to(torch.int64)
+    dw = ds = 0
+    for o in range(0, v.numel(), chunk):
+        c = v[o:o + chunk]
+        w = torch.arange(o, o + c.numel(), dtype=torch.int64, device=c.device) * -7046029254386353131 + 1
+        dw += int((c * w).sum())
+        ds += int((c ^ (c >> 29)).sum())
+    return dw & MASK64, ds & MASK64
+
+
+def dft_bins(x, ks):
+    """Direct DFT bins X[k] = sum_n x[n] w^{nk} (w = e^{-2 pi i/N}) of a
+    complex128 device vector of N = 2^L points, in float64 with exact integer
+    phases mod N: n = a + 2^h b, X[k] = sum_a w^{ak} sum_b x[b, a] w^{2^h b k}
+    -- one (K x 2^h) x (2^h x 2^(L-h)) GEMM over the resident input (no copy of
+    it).  Independent of the FFT (bench.py's check of config 5, whose size the
+    reference cannot express)."""
+    import math
+    import torch
+    n = x.numel()
+    logn = n.bit_length() - 1
+    h = logn // 2
+    A, B = 1 << h, n >> h
+    k = torch.tensor(list(ks), dtype=torch.int64, device=x.device)[:, None]
+    mask = n - 1
+    b = torch.arange(B, dtype=torch.int64, device=x.device)[None, :]
+    ang = (((b << h) * k) & mask).to(torch.float64) * (-2.0 * math.pi / n)
+    wb = torch.polar(torch.ones_like(ang), ang)
+    y = wb @ x.view(B, A)  # (K, A): sum_b x[b, a] w^{2^h b k}
+    a = torch.arange(A, dtype=torch.int64, device=x.device)[None, :]
+    ang = ((a * k) & mask).to(torch.float64) * (-2.0 * math.pi / n)
+    wa = torch.polar(torch.ones_like(ang), ang)
+    return (y * wa).sum(dim=1)
+
+
+def sample_bins(n: int, workers: int, per_worker: int = 8) -> list[int]:
+    """Natural-order bins to check directly: per_worker of each worker's bins
+    bitrev(q) + P k (its first, second, middle and last k, and spread ones)."""
+    m = n // workers
+    bits = workers.bit_length() - 1
+    ks = sorted({0, 1, m // 2, m - 1} | {(j * 0x9E3779B1 + 7) % m for j in range(max(0, per_worker - 4))})[:per_worker]
+    return [bitrev(q, bits) + workers * k for q in range(workers) for k in ks]
+
+
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist

@@ -166,7 +166,8 @@ int pifft_execute_device_timed(pifft_plan* plan, const void* d_in, void* d_out, 
  * 2 + 3: 2.92 ms in the fast state, 3.13-3.5 ms in the slow one; DESIGN.md
  * section 4).  This call times the plan on (d_in, d_out) with its current W,
  * then with up to tries - 1 freshly allocated ones, and keeps the fastest (one
- * extra W at a time; stops early if it cannot allocate).  *best_ms (may be
+ * extra W at a time, every loser kept until the call returns; stops early
+ * when the device would keep less than another W and 4 GiB free).  *best_ms (may be
  * NULL) receives the kept workspace's mean execution time.  Synchronous.
  * Results are unchanged; only timings move. */
 int pifft_plan_tune_workspace(pifft_plan* plan, const void* d_in, void* d_out, void* stream, int tries,
@@ -201,8 +202,9 @@ int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int* launch_sampl
  * CPU.c:496-499).  A PIFFT_OUT_BITREV plan instead writes its workers'
  * scratch segments at host_out[b N + q M + i] (the reference's tmp_in
  * layout, q = first..first+count-1).  ms_stage1 / ms_stage2 receive the
- * device time of the tree stage and of the rest (the reference's two timers,
- * CPU.c:414-481).  When a plan evaluates its tree inside the first local-FFT
+ * device wall time of the tree stage and of the rest, from a marker event
+ * before each stage's first launch to one after its last (the reference's
+ * two stage timers, CPU.c:414-481: gaps between launches count).  When a plan evaluates its tree inside the first local-FFT
  * pass (one worker per plan, log2 P <= 4, a multi-pass local FFT; see
  * pifft_plan_info.launch_kind 4) that fused launch cannot be split: stage 1 is
  * then the tree PLUS the first pass, and stage 2 the remaining passes
@@ -220,6 +222,14 @@ int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double*
  * the host. */
 int pifft_execute_group(pifft_plan** plans, int nplans, const void* host_in, void* host_out,
                         double* ms_stage1, double* ms_stage2);
+
+/* Kernel-only stage times: re-runs the plans of the last pifft_execute_group
+ * call on their staged input (no host copies) with events bound to every
+ * launch, and returns the summed kernel durations of the tree stage and of
+ * the rest for the slowest plan -- pifft_execute_group's wall stage times
+ * minus the gaps between launches (CLI -x extra columns). */
+int pifft_execute_group_kernel_times(pifft_plan** plans, int nplans, double* kernel_ms_stage1,
+                                     double* kernel_ms_stage2);
 
 /* The optional final exchange of a multi-GPU job (the
  * reference's counterpart is every worker writing its bins into the shared

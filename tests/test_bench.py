@@ -91,6 +91,10 @@ def test_bench_gpus_2_spawns_two_ranks():
         assert "error" not in rec, (key, rec)
         assert rec["value"] > 0 and rec["n_gpus"] == 2
     assert sec["C3_batch"]["batch_per_gpu"] == 2048
+    # the split checks itself: slices bitwise vs rank 0's replay, the gathered result vs one GPU
+    v = d["config"]["verify"]
+    assert v["ok"] and v["slices_bitwise"] and v["slices_checked"] == 2 and v["rel_l2"] <= 1e-12, v
+    assert sec["C2_split"]["verify"]["ok"], sec["C2_split"]["verify"]
 
 
 def test_bench_gpus_8_rehearsal_config5():
@@ -111,6 +115,12 @@ def test_bench_gpus_8_rehearsal_config5():
     for key in ("C2_split", "C3_batch"):
         _roofline_ok(sec[key]["roofline_rank0"])
     _roofline_ok(sec["C5"]["roofline_rank0"])
+    # self-verification of every worker split (round-3 verdict: the first 8-GPU run proves itself)
+    v = d["config"]["verify"]
+    assert v["ok"] and v["slices_bitwise"] and v["slices_checked"] == 8 and v["rel_l2"] <= 1e-12, v
+    assert sec["C2_split"]["verify"]["ok"] and sec["C5"]["verify"]["ok"], (sec["C2_split"]["verify"], sec["C5"]["verify"])
+    assert sec["C5"]["verify"]["slices_bitwise"] and sec["C5"]["verify"]["rel_l2"] <= 1e-12
+    assert v["bins_ok"] and sec["C5"]["verify"]["bins_ok"] and sec["C5"]["verify"]["bins"] == 64
 
 
 def test_bench_config5_hbm_check_refuses_cleanly():

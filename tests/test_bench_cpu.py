@@ -43,25 +43,42 @@ def test_reference_touched_memory_model():
     assert vals == sorted(vals)
 
 
-@pytest.mark.parametrize("avail_gib,cpus,threads,log_n,esz,want", [
-    (2900, 256, None, 28, 16, 32),  # the GPU box: p_to = 32 (196 GiB) under the per-command cap
-    (2900, 256, 16, 28, 16, 16),    # --cpu-threads 16
-    (100, 256, None, 28, 16, 8),    # 72 GiB budget: p = 8 touches 52 GiB, p = 16 100 GiB
-    (2900, 8, None, 28, 16, 8),     # 8 online CPUs: how_many_cores caps p (CPU.c:200)
-    (64, 8, 8, 20, 16, 8),          # small N: the thread count decides
-    (1024, 256, 1, 20, 16, 1),
+@pytest.mark.parametrize("avail_gib,cpus,share,threads,log_n,esz,want", [
+    (2900, 256, 16, None, 28, 16, 16),  # the GPU box: 256 online CPUs, a 16-CPU cgroup quota -> p = 16
+    (2900, 256, 256, None, 28, 16, 32),  # no quota: the reference's p_to = 32 (196 GiB) under the per-command cap
+    (2900, 256, 16, 32, 28, 16, 32),    # --cpu-threads 32
+    (100, 256, 256, None, 28, 16, 8),   # 72 GiB budget: p = 8 touches 52 GiB, p = 16 100 GiB
+    (2900, 8, 8, None, 28, 16, 8),      # 8 online CPUs: how_many_cores caps p (CPU.c:200)
+    (64, 8, 8, 8, 20, 16, 8),           # small N: the thread count decides
+    (1024, 256, 256, 1, 20, 16, 1),
 ])
-def test_reference_worker_count(monkeypatch, avail_gib, cpus, threads, log_n, esz, want):
+def test_reference_worker_count(monkeypatch, avail_gib, cpus, share, threads, log_n, esz, want):
     monkeypatch.setattr(bench, "_mem_available", lambda: avail_gib << 30)
     monkeypatch.setattr(bench, "_cgroup_mem_limit", lambda: None)
     monkeypatch.setattr(bench.os, "cpu_count", lambda: cpus)
+    monkeypatch.setattr(bench, "_cpu_share", lambda: share)
     assert bench.ref_workers(log_n, esz, threads) == want
+    # the reference's own rule (online CPUs only) for the line's "alternative"
+    if threads is None and cpus >= 32 and avail_gib > 1000:
+        assert bench.ref_workers(log_n, esz, share=False) == 32
+
+
+def test_cpu_share_follows_the_cgroup_quota(monkeypatch):
+    monkeypatch.setattr(bench.os, "cpu_count", lambda: 256)
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(bench, "_cgroup_cpu_quota", lambda: 16.0)
+    assert bench._cpu_share() == 16
+    monkeypatch.setattr(bench, "_cgroup_cpu_quota", lambda: None)
+    assert bench._cpu_share() == 256
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(12)))
+    assert bench._cpu_share() == 12
 
 
 def test_reference_worker_count_follows_cgroup_limit(monkeypatch):
     monkeypatch.setattr(bench, "_mem_available", lambda: 2900 << 30)
     monkeypatch.setattr(bench, "_cgroup_mem_limit", lambda: 110 << 30)  # 91 GiB budget: p = 16 touches 100
     monkeypatch.setattr(bench.os, "cpu_count", lambda: 256)
+    monkeypatch.setattr(bench, "_cpu_share", lambda: 256)
     assert bench.ref_workers(28, 16) == 8
 
 

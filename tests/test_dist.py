@@ -140,3 +140,102 @@ def test_batch_range():
         pifft_dist.batch_range(0, 3, 4096)
     with pytest.raises(ValueError):
         pifft_dist.batch_range(0, 2, 0)
+
+
+# ------------------------------------------------ multi-GPU self-verification ---
+def _digest_rank_main(rank, world, port, q_out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "cs87project-msolano2_amd"))
+    import pifft_dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(5)
+        t = torch.randn(3000, dtype=torch.complex128, generator=g)
+        if rank == 1:
+            t = t.clone()
+        digests = [None] * world
+        dist.all_gather_object(digests, pifft_dist.tensor_digest(t, chunk=512))
+        if rank == 0:
+            q_out.put(all(tuple(d) == pifft_dist.tensor_digest(t) for d in digests))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_slice_digests_agree():
+    """bench.py's slices_bitwise check: each rank's integer digest, gathered
+    with all_gather_object (gloo), equals rank 0's for the same bits, and the
+    digest does not depend on the chunking."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_digest_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get()
+
+
+def test_tensor_digest_sees_every_bit():
+    import pifft_dist
+    x = torch.randn(1 << 12, dtype=torch.complex128)
+    d0 = pifft_dist.tensor_digest(x)
+    assert pifft_dist.tensor_digest(x.clone(), chunk=100) == d0
+    for pos in (0, 777, (1 << 12) - 1):
+        y = torch.view_as_real(x.clone()).reshape(-1).view(torch.int64)
+        y[2 * pos + 1] ^= 1  # the lowest mantissa bit of one imaginary part
+        assert pifft_dist.tensor_digest(torch.view_as_complex(y.view(torch.float64).view(-1, 2))) != d0
+    a = x.clone()
+    a[[3, 4]] = a[[4, 3]]  # two values swapped: same multiset, different positions
+    assert pifft_dist.tensor_digest(a) != d0
+    f = torch.randn(1000, dtype=torch.complex64)
+    assert pifft_dist.tensor_digest(f) == pifft_dist.tensor_digest(f.clone())
+
+
+def test_direct_bins_match_fft_and_sample_ownership():
+    import pifft_dist
+    n, P = 1 << 12, 8
+    x = torch.randn(n, dtype=torch.complex128)
+    ks = pifft_dist.sample_bins(n, P)
+    assert len(ks) == 8 * P and len(set(ks)) == len(ks)
+    # each worker's bins are its own residue class bitrev(q) + P k
+    for q in range(P):
+        r = pifft_dist.bitrev(q, 3)
+        assert all(k % P == r for k in ks[8 * q:8 * (q + 1)])
+    want = np.fft.fft(x.numpy())[ks]
+    got = pifft_dist.dft_bins(x, ks).numpy()
+    assert np.max(np.abs(got - want)) <= 1e-12 * np.linalg.norm(want)
+
+
+def test_verify_finish_accepts_and_rejects():
+    """bench.py verify_finish (rank 0): rel-L2 against the one-GPU reference,
+    direct bins against a misplaced bin, and the slice check's verdict."""
+    import bench
+    import pifft_dist
+    n, P = 1 << 12, 4
+    x = torch.randn(n, dtype=torch.complex128) / 64
+    X = torch.fft.fft(x)
+    ks = pifft_dist.sample_bins(n, P)
+    good = {"slices_bitwise": True, "slices_checked": P, "slices_differing": [], "tol": 1e-12,
+            "reference": "test", "ref": X.clone()}
+    v = bench.verify_finish(torch, good, X * (1 + 1e-15))
+    assert v["ok"] and v["rel_l2"] <= 1e-12 and v["bins_ok"] is None
+    bad = X.clone()
+    bad[[5, 9]] = bad[[9, 5]]  # two bins swapped: a permutation fault
+    assert not bench.verify_finish(torch, good, bad)["ok"]
+    assert not bench.verify_finish(torch, dict(good, slices_bitwise=False), X)["ok"]
+    binsprep = {"slices_bitwise": True, "tol": 1e-12, "ks": ks, "bins": pifft_dist.dft_bins(x, ks),
+                "x_norm": float(torch.linalg.vector_norm(x)), "reference": "bins"}
+    v = bench.verify_finish(torch, binsprep, X)
+    assert v["ok"] and v["bins_ok"] and v["bins"] == len(ks) and v["rel_l2"] is None
+    moved = X.clone()
+    moved[ks[3]] = X[ks[3] + P]  # a neighbouring bin of the same worker in its place
+    assert not bench.verify_finish(torch, binsprep, moved)["bins_ok"]
+    v = bench.verify_finish(torch, good, None)
+    assert v["ok"] and v["rel_l2"] is None and "slices only" in v["note"]
+    assert bench.verify_finish(torch, {}, X) is None  # ranks other than 0
