@@ -527,7 +527,8 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
     }
     // tuning: lines per workgroup of the last pass (its write side's segment width)
     const int last_c = env_int("PIFFT_LAST_C", 0);
-    if (last_c > 0 && out.size() > 1 && find_pass(prec, out.back().R, last_c, out.back().mode, out.back().nts))
+    if (last_c > 0 && out.size() > 1 &&
+        find_pass(prec, out.back().R, last_c, out.back().mode, out.back().nts, 0, out.back().vpt))
         out.back().C = last_c;
     return 0;
 }

@@ -15,7 +15,6 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
-os.environ["PIFFT_TUNING"] = "1"  # libpifft reads the variants' PIFFT_* variables only then
 
 
 def main():
@@ -59,6 +58,7 @@ def main():
         for k in [k for k in os.environ if k.startswith("PIFFT_")]:
             del os.environ[k]
         os.environ.update({k: str(v) for k, v in var.items()})
+        os.environ["PIFFT_TUNING"] = "1"
         count = args.count or args.workers
         plan = pifft.Plan(n, args.workers, args.batch, prec, first=args.first, count=count, device=0,
                           flags=None if args.flags < 0 else args.flags)
