@@ -30,7 +30,14 @@
  * the wall total, then the kernel-only stage sums: stage times without the
  * gaps between launches),
  * -W untimed warm-up runs before the timed one (default 1; code-object load),
- * -l list GPUs (the how-many-* utilities).  -n is parsed as 64-bit.
+ * -l list GPUs (the how-many-* utilities), -R rehearse a -g split with every
+ * plan on GPU 0 (a one-GPU box runs the multi-plan path).  -n is parsed as
+ * 64-bit.
+ *
+ * -t with -g G > 1 also checks the split itself: the G-plan result against a
+ * one-GPU all-worker plan of the same input (rel-L2 within the north star's
+ * tolerance) and every plan's bins against the same worker range replayed on
+ * GPU 0 (bit for bit) -- the multi-GPU path proving its own output.
  */
 #define _GNU_SOURCE
 #include <math.h>
@@ -63,12 +70,13 @@ typedef struct tr {
     int warmups;         /* -W */
     int bitrev;          /* -r */
     int separate_tree;   /* -u */
+    int rehearse;        /* -R */
 } tr_t;
 
 static void show_usage(void) {
     print_out("\nusage:\n"
               "  pifft { -n <n> -p <p> [-o] | -t } [-f 32|64] [-b <batch>] [-s <seed>]\n"
-              "        [-g <gpus>] [-w <file>] [-r] [-u] [-x] [-W <warmups>] [-l]\n"
+              "        [-g <gpus>] [-w <file>] [-r] [-u] [-x] [-W <warmups>] [-l] [-R]\n"
               "\noptions:\n"
               "  -n <n>     power of two input size\n"
               "  -p <p>     power of two number of processors (less than n)\n"
@@ -84,6 +92,7 @@ static void show_usage(void) {
               "  -x         extra columns: GFLOP/s, algorithmic GB/s, kernel-only stage 1 / 2 ms\n"
               "  -W <w>     untimed warm-up runs (default 1)\n"
               "  -l         list GPUs and exit\n"
+              "  -R         rehearse the -g split with every plan on GPU 0\n"
               "\n");
 }
 
@@ -119,7 +128,7 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
     t->batch = 1;
     t->gpus = 1;
     t->warmups = 1;
-    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:ruxW:l")) != -1) {
+    while ((ret = getopt(argc, argv, "n:p:tof:b:s:g:w:ruxW:lR")) != -1) {
         switch (ret) {
             case 'n':
                 if (parse_u64(optarg, &num) || !(num > 1) || !is_power_of_two_u64(num)) {
@@ -187,6 +196,9 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
             case 'x':
                 t->extra = 1;
                 break;
+            case 'R':
+                t->rehearse = 1;
+                break;
             case 'W':
                 if (parse_u64(optarg, &num) || num > 1000) {
                     stderr_out("Invalid warm-up count\n");
@@ -230,7 +242,7 @@ int setup_from_args(tr_t* t, int argc, char** argv) {
             stderr_out("No GPU available (%s)\n", pifft_last_error());
             goto err;
         }
-        if (t->gpus > (uint32_t)ngpu) {
+        if (t->gpus > (uint32_t)ngpu && !t->rehearse) {
             stderr_out("Too many GPUs! (only %d GPUs available)\n", ngpu);
             goto err;
         }
@@ -323,6 +335,71 @@ static void cleanup_data(tr_t* t) {
     t->in = t->out = NULL;
 }
 
+static int device_of(const tr_t* t, uint32_t g) { return t->rehearse ? 0 : (int)g; }
+
+/* -t with -g G > 1: the split checks itself (see the header).  Returns 0 when
+ * both checks pass, 1 when one fails, -1 on an error. */
+static int check_split(const tr_t* t, pifft_plan* const* plans) {
+    const uint64_t total = t->N * (uint64_t)t->batch;
+    const uint32_t G = t->gpus, per = t->P / G;
+    void* ref = calloc(total, esz(t));
+    void* rep = malloc(total * esz(t));
+    pifft_plan* one = NULL;
+    int rc = -1;
+    if (!ref || !rep) goto out;
+    /* the whole transform on GPU 0, all P workers (same order as the split) */
+    if (pifft_plan_create_slices(&one, t->N, t->P, 0, t->P, t->batch, t->prec, 0,
+                                 t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_NATURAL) ||
+        pifft_execute(one, t->in, ref, NULL, NULL)) {
+        stderr_out("%s\n", pifft_last_error());
+        goto out;
+    }
+    pifft_plan_destroy(one);
+    one = NULL;
+    double num = 0, den = 0;
+    for (uint64_t i = 0; i < total; i++) {
+        const double dr = re_at(t, t->out, i) - re_at(t, ref, i), di = im_at(t, t->out, i) - im_at(t, ref, i);
+        num += dr * dr + di * di;
+        den += re_at(t, ref, i) * re_at(t, ref, i) + im_at(t, ref, i) * im_at(t, ref, i);
+    }
+    const double err = den > 0 ? sqrt(num / den) : sqrt(num);
+    const double tol = t->prec == PIFFT_F64 ? 1e-12 : 1e-5 * log2((double)t->N);
+    /* every plan's worker range again, on GPU 0: its bins bit for bit */
+    int same = 1;
+    for (uint32_t g = 0; g < G && same; g++) {
+        memset(rep, 0xff, total * esz(t));  /* NaN pattern: positions the plan does not write */
+        pifft_plan* p = NULL;
+        if (pifft_plan_create_slices(&p, t->N, t->P, g * per, per, t->batch, t->prec, 0,
+                                     t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_SLICES) ||
+            pifft_execute(p, t->in, rep, NULL, NULL)) {
+            stderr_out("%s\n", pifft_last_error());
+            if (p) pifft_plan_destroy(p);
+            goto out;
+        }
+        pifft_plan_destroy(p);
+        const size_t e = esz(t);
+        uint64_t written = 0;
+        for (uint64_t i = 0; i < total && same; i++) {
+            static const unsigned char nanpat[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                                     0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+            const char* a = (const char*)rep + i * e;
+            if (!memcmp(a, nanpat, e)) continue;
+            written++;
+            same = !memcmp(a, (const char*)t->out + i * e, e);
+        }
+        same = same && written == total / G;
+    }
+    print_out("Split check (%u plans vs one GPU): rel-L2 %.3e (tolerance %.1e), worker ranges replayed bit for bit: %s\n",
+              G, err, tol, same ? "yes" : "NO");
+    print_out(err <= tol && same ? "Split check passed.\n\n" : "Split check FAILED.\n\n");
+    rc = err <= tol && same ? 0 : 1;
+out:
+    if (one) pifft_plan_destroy(one);
+    free(ref);
+    free(rep);
+    return rc;
+}
+
 /* CPU.c:312-380: the P workers go to t->gpus GPUs, P/gpus consecutive workers
  * each, and run concurrently; no data moves between GPUs. */
 int run(tr_t* t) {
@@ -337,7 +414,7 @@ int run(tr_t* t) {
         int r = (G == 1) ? pifft_plan_create_slices(&plans[g], t->N, t->P, 0, t->P, t->batch, t->prec, 0,
                                                     (t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_NATURAL) | sep)
                          : pifft_plan_create_slices(&plans[g], t->N, t->P, g * per, per, t->batch, t->prec,
-                                                    (int)g, (t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_SLICES) | sep);
+                                                    device_of(t, g), (t->bitrev ? PIFFT_OUT_BITREV : PIFFT_OUT_SLICES) | sep);
         if (r) {
             stderr_out("(GPU %u): %s\n", g, pifft_last_error());
             goto done;
@@ -378,6 +455,7 @@ int run(tr_t* t) {
     } else {
         print_output(t);
         verify_results(t);
+        if (G > 1 && check_split(t, plans) < 0) goto done;
     }
     if (t->dump) {
         FILE* f = fopen(t->dump, "wb");

@@ -1041,22 +1041,35 @@ void stage_split(const pifft_plan* p, const std::vector<float>& ms, double* s1, 
 // event before the stage's first launch and after its last, so the gaps and
 // launch latency between kernels count.  (The stage-1 launches -- the tree,
 // or the tree fused into the first pass -- lead every plan.)
+// An empty stage (P = 1: no tree, as the reference's funnel loop that never
+// runs; M = 1: no local FFT) gets no marker of its own and reads 0.
+size_t stage1_launches(const pifft_plan* p) {
+    size_t n1 = 0;
+    while (n1 < p->steps.size() && stage1_step(p->steps[n1])) n1++;
+    return n1;
+}
 int launch_stage_marked(pifft_plan* p, const void* d_in, void* d_out) {
+    const size_t n1 = stage1_launches(p), ns = p->steps.size();
     HIPCHK(hipEventRecord(p->sev[0], p->stream));
-    size_t i = 0;
-    for (; i < p->steps.size() && stage1_step(p->steps[i]); i++)
+    for (size_t i = 0; i < ns; i++) {
+        if (i == n1 && n1 > 0) HIPCHK(hipEventRecord(p->sev[1], p->stream));
         if (launch_step(p, p->steps[i], d_in, d_out, p->stream)) return -1;
-    HIPCHK(hipEventRecord(p->sev[1], p->stream));
-    for (; i < p->steps.size(); i++)
-        if (launch_step(p, p->steps[i], d_in, d_out, p->stream)) return -1;
+    }
     HIPCHK(hipEventRecord(p->sev[2], p->stream));
     return 0;
 }
 int read_stage_marked(pifft_plan* p, double* s1, double* s2) {
+    const size_t n1 = stage1_launches(p), ns = p->steps.size();
     float a = 0.0f, b = 0.0f;
     HIPCHK(hipEventSynchronize(p->sev[2]));
-    HIPCHK(hipEventElapsedTime(&a, p->sev[0], p->sev[1]));
-    HIPCHK(hipEventElapsedTime(&b, p->sev[1], p->sev[2]));
+    if (n1 == 0)
+        HIPCHK(hipEventElapsedTime(&b, p->sev[0], p->sev[2]));
+    else if (n1 == ns)
+        HIPCHK(hipEventElapsedTime(&a, p->sev[0], p->sev[2]));
+    else {
+        HIPCHK(hipEventElapsedTime(&a, p->sev[0], p->sev[1]));
+        HIPCHK(hipEventElapsedTime(&b, p->sev[1], p->sev[2]));
+    }
     *s1 = a;
     *s2 = b;
     return 0;

@@ -477,6 +477,36 @@ def test_cli_tsv_and_dump(tmp_path):
         assert_bins_close(got, oracle.fft(x, P=4)[_bitrev_perm(4096)], "f64", 4096)
 
 
+def test_cli_extra_columns_kernel_and_wall_stages():
+    """-x: GFLOP/s, GB/s and the kernel-only stage sums beside the wall-clock
+    stage timers (markers around each stage, the reference's tm_funnel /
+    tm_tube, CPU.c:414-481): the kernels fit inside the wall stage times."""
+    for args in (["-n", "1048576", "-p", "8", "-f", "64"], ["-n", "1048576", "-p", "8", "-f", "64", "-u"],
+                 ["-n", "1048576", "-p", "1", "-f", "64"]):
+        r = _cli(args + ["-x", "-W", "3"])
+        assert r.returncode == 0, r.stderr
+        head, vals = r.stdout.strip().splitlines()[-2:]
+        assert head.split("\t")[-2:] == ["kernels (stage 1)", "kernels (stage 2)"]
+        c = [float(v) for v in vals.split("\t")]
+        assert len(c) == 9 and abs(c[2] - c[3] - c[4]) < 1e-3
+        assert c[7] >= 0 and c[8] > 0 and c[7] + c[8] <= 1.2 * c[2] + 0.005, c
+        if args[3] == "1":
+            assert c[3] == 0 and c[7] == 0  # P = 1: no tree stage
+
+
+@pytest.mark.parametrize("args", [["-f", "64", "-p", "8", "-g", "4"], ["-f", "32", "-p", "8", "-g", "8"],
+                                  ["-f", "64", "-p", "4", "-g", "2", "-r"], ["-f", "64", "-p", "16", "-g", "4", "-b", "3"]])
+def test_cli_split_checks_itself(args):
+    """-t with -g G > 1 (rehearsed on GPU 0, -R): the split's result against a
+    one-GPU all-worker plan (rel-L2) and each plan's worker range replayed on
+    GPU 0 bit for bit.  -n after -t transforms 4096 points (the reference's
+    quirk: its N = 8 known answer then fails, the split check still runs)."""
+    r = _cli(["-t", "-n", "4096"] + args + ["-R"])
+    assert r.returncode == 0, r.stderr
+    assert "Split check passed." in r.stdout, r.stdout[-400:]
+    assert "replayed bit for bit: yes" in r.stdout
+
+
 @pytest.mark.parametrize("P", ["1", "2", "8"])
 def test_cli_known_answer_scratch_order(P):
     r = _cli(["-t", "-p", P, "-r"])
