@@ -1,0 +1,17 @@
+#!/bin/bash
+# tools/gpu_r04c.sh -- round-4 session c: PMC traffic of the C4 / C4_f32 / C3
+# plans (tools/gpu_r04.sh stage p), then A/B sweeps of the fp32 2^28 last pass
+# (XCD tile grouping, streaming form, workspace row pad) and config 2's
+# one-GPU slice with the tree unfused.
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r04c
+mkdir -p "$out"
+bash tools/gpu_r04.sh r04c p || exit 1
+timeout -k 10 300 python3 -u tools/tune.py --log-n 28 --prec 32 --tune-ws 8 --steps 20 --variants \
+  '[{}, {"PIFFT_LAST_XCD_GROUP": 0}, {"PIFFT_LAST_XCD_GROUP": 1}, {"PIFFT_LAST_XCD_GROUP": 3}, {"PIFFT_LAST_XCD_GROUP": 4}, {"PIFFT_LAST_NT": 0}, {"PIFFT_W_PAD": 0}, {"PIFFT_W_PAD": 1056}, {"PIFFT_W_PAD": 4128}, {}]' \
+  > "$out/fp32_last_pass_sweep.log" 2>&1 || { tail "$out/fp32_last_pass_sweep.log"; exit 1; }
+cat "$out/fp32_last_pass_sweep.log"
+timeout -k 10 120 python3 -u tools/tune.py --log-n 20 --prec 64 --workers 8 --first 0 --count 1 --steps 200 --warmup 20 --variants \
+  '[{}, {"PIFFT_FUSE_TREE": 0}, {}, {"PIFFT_FUSE_TREE": 0}]' > "$out/c2_slice_unfused.log" 2>&1 || { tail "$out/c2_slice_unfused.log"; exit 1; }
+cat "$out/c2_slice_unfused.log"
