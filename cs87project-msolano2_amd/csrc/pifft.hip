@@ -525,6 +525,17 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             pc.vpt = 32;
         }
     }
+    // tuning: strided passes (and the fused tree pass) at PIFFT_STRIDED_VPT
+    // values per thread where that instance exists (8: radix-8 stages, twice
+    // the waves per workgroup)
+    {
+        const int svpt = env_int("PIFFT_STRIDED_VPT", 0);
+        for (auto& pc : out)
+            if (svpt > 0 && (pc.mode == 1 || pc.mode == 2) &&
+                find_pass(prec, pc.R, pc.C, (pc.mode == 1 && heavy_lp) ? 3 : pc.mode, pc.nts,
+                          pc.mode == 1 ? heavy_lp : 0, svpt))
+                pc.vpt = svpt;
+    }
     // tuning: lines per workgroup of the last pass (its write side's segment width)
     const int last_c = env_int("PIFFT_LAST_C", 0);
     if (last_c > 0 && out.size() > 1 &&
@@ -686,7 +697,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // tree launch that writes, and a pass that re-reads, the N/P segment).
     const PassKernel* fused = nullptr;
     if (may_fuse && passes.size() > 1)
-        fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp);
+        fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp, passes[0].vpt);
     p->fused_tree = fused != nullptr;
 
     // --- chain: [tree] [passes] [interleave] ---

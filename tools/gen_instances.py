@@ -72,6 +72,13 @@ for R in (512, 1024):
     for nts in (0, 1):
         for mode in (1, 2):
             items.append(f"PKV(float, 32, {R}, {C}, {mode}, {nts}, 0, 32),")
+# fp64 strided passes at 8 values per thread (radix-8 stages, twice the waves
+# per workgroup) for the latency-bound 2^20 configs: config 1's two 1024-point
+# passes at C = 4 and config 2's one-GPU slice (the fused tree + 512-point pass,
+# the 256-point pass), PIFFT_STRIDED_VPT=8 (tuning, round 4)
+for R, C, mode, lp in ((1024, 4, 1, 0), (1024, 4, 2, 0), (512, 4, 3, 3), (256, 4, 2, 0)):
+    for nts in (0, 1):
+        items.append(f"PKV(double, 64, {R}, {C}, {mode}, {nts}, {lp}, 8),")
 # (a 32768-value tile -- C = 32 at R = 1024, one 1024-thread workgroup per CU,
 # 256-B segments -- made the fp32 2^28 last pass 0.88 -> 1.07 ms: round 4,
 # profiles/r04_fp32_last_pass_c32.log; not instantiated)

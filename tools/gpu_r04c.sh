@@ -15,3 +15,7 @@ cat "$out/fp32_last_pass_sweep.log"
 timeout -k 10 120 python3 -u tools/tune.py --log-n 20 --prec 64 --workers 8 --first 0 --count 1 --steps 200 --warmup 20 --variants \
   '[{}, {"PIFFT_FUSE_TREE": 0}, {}, {"PIFFT_FUSE_TREE": 0}]' > "$out/c2_slice_unfused.log" 2>&1 || { tail "$out/c2_slice_unfused.log"; exit 1; }
 cat "$out/c2_slice_unfused.log"
+# the radix-4 cross-lane last stage (v_permlane32/16_swap, PIFFT_PERMLANE=3) vs the default (radix 2 only)
+AB_ROUNDS=2 timeout -k 10 300 bash tools/ab.sh "--log-n 28 --prec 64 --tune-ws 8 --steps 20" abvar/base.so abvar/perm3.so > "$out/permlane4_c4.log" 2>&1 || { tail "$out/permlane4_c4.log"; exit 1; }
+AB_ROUNDS=2 timeout -k 10 200 bash tools/ab.sh "--log-n 20 --prec 64 --steps 400 --warmup 20" abvar/base.so abvar/perm3.so > "$out/permlane4_c1.log" 2>&1 || { tail "$out/permlane4_c1.log"; exit 1; }
+grep -v "^torch" "$out/permlane4_c4.log" "$out/permlane4_c1.log"
