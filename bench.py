@@ -531,10 +531,15 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             # means hold to ~1 % against the rocprofv3 trace
             job.time_launches(200 if g["log_n"] < 24 else max(5, k // 2))
             flops = 5.0 * n * g["log_n"] * g["batch"]
+            rf = job.roofline(ms)
+            # PMC traffic of this very plan's dominant kernel, when a committed summary profiled it
+            key = f"n2^{g['log_n']}_f{32 if g['prec'] == F32 else 64}_b{g['batch']}_P{g['P']}_q{g['count']}"
+            rf["traffic"], rf["traffic_source"] = load_traffic(key, rf["launches"],
+                                                               [job.plan.kernel_name(i) for i in rf["launches"]])
             rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
                         "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],
                         "workers_in_plan": g["count"], "batch": g["batch"], "passes": job.desc["num_passes"],
-                        "radix": job.desc["radix"], "launches": job.launches(ms), "roofline": job.roofline(ms)})
+                        "radix": job.desc["radix"], "launches": job.launches(ms), "roofline": rf})
             job.free()
         except Exception as e:  # reported, never silently replaced
             rec["error"] = repr(e)

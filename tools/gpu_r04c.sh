@@ -19,3 +19,9 @@ cat "$out/c2_slice_unfused.log"
 AB_ROUNDS=2 timeout -k 10 300 bash tools/ab.sh "--log-n 28 --prec 64 --tune-ws 8 --steps 20" abvar/base.so abvar/perm3.so > "$out/permlane4_c4.log" 2>&1 || { tail "$out/permlane4_c4.log"; exit 1; }
 AB_ROUNDS=2 timeout -k 10 200 bash tools/ab.sh "--log-n 20 --prec 64 --steps 400 --warmup 20" abvar/base.so abvar/perm3.so > "$out/permlane4_c1.log" 2>&1 || { tail "$out/permlane4_c1.log"; exit 1; }
 grep -v "^torch" "$out/permlane4_c4.log" "$out/permlane4_c1.log"
+# strided passes at 8 values per thread (twice the waves) on the latency-bound 2^20 configs
+timeout -k 10 120 python3 -u tools/tune.py --log-n 20 --prec 64 --steps 400 --warmup 20 --variants \
+  '[{}, {"PIFFT_STRIDED_VPT": 8}, {}, {"PIFFT_STRIDED_VPT": 8}]' > "$out/vpt8_c1.log" 2>&1 || { tail "$out/vpt8_c1.log"; exit 1; }
+timeout -k 10 120 python3 -u tools/tune.py --log-n 20 --prec 64 --workers 8 --first 0 --count 1 --steps 400 --warmup 20 --variants \
+  '[{}, {"PIFFT_STRIDED_VPT": 8}, {}, {"PIFFT_STRIDED_VPT": 8}]' > "$out/vpt8_c2_slice.log" 2>&1 || { tail "$out/vpt8_c2_slice.log"; exit 1; }
+grep -v "^torch" "$out/vpt8_c1.log" "$out/vpt8_c2_slice.log"

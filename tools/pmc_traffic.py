@@ -7,8 +7,12 @@ Recipe (MI355X_MICROARCH.md, HBM / rocprofv3 PMC slots):
     --pmc);
   * gfx950 correction: FETCH_SIZE reports exactly half of the bytes of a wide
     (16 B/lane) coalesced streaming read -> x2 for the fp64 kernels here;
-    WRITE_SIZE is exact for 16 B/lane streaming stores.  (8 B/lane fp32
-    accesses are uncalibrated: reported uncorrected, flagged.)
+    WRITE_SIZE is exact for 16 B/lane streaming stores.  The fp32 kernels'
+    8 B/lane reads are calibrated on the fp32 2^28 plan (round 4,
+    profiles/r04c_traffic_n2^28_f32_b1_P1_q1.json): each pass streams 2 GiB in,
+    8x the Infinity Cache, so every input byte must come from memory at least
+    once, yet raw FETCH_SIZE is 0.500x those bytes in all three passes -- the
+    same half count -> x2 as well (WRITE_SIZE: 1.000x, exact).
 
 Runs bench.py under each counter pass, maps the timed loop's dispatches to
 the plan's launch indices (the plan's launches repeat in order every step),
@@ -69,7 +73,29 @@ def per_dispatch(rows: list[dict], counter: str) -> list[tuple[int, str, float]]
     return [(d, acc[d][0], acc[d][1]) for d in sorted(acc)]
 
 
+def correction(prec: int) -> str:
+    return ("FETCH_SIZE KiB x1024 x2 (gfx950 16 B/lane streaming read), WRITE_SIZE KiB x1024" if prec == 64 else
+            "FETCH_SIZE KiB x1024 x2 (gfx950 8 B/lane streaming read: half-counted, calibrated on the fp32 2^28 "
+            "passes -- raw 0.500x the compulsory bytes of a stream 8x the Infinity Cache), WRITE_SIZE KiB x1024")
+
+
+def recorrect(path: str, out: str) -> None:
+    """Rewrites a summary with the current correction (the raw counter values
+    are kept in every summary)."""
+    d = json.load(open(path))
+    prec = int(d["config_key"].split("_f")[1].split("_")[0])
+    for i, k in d["kernels"].items():
+        k["fetch_bytes_corrected"] = k["FETCH_SIZE_KiB"] * 1024 * 2
+        k["write_bytes"] = k["WRITE_SIZE_KiB"] * 1024
+        d["per_launch_bytes"][i] = k["fetch_bytes_corrected"] + k["write_bytes"]
+    d["correction"] = correction(prec)
+    with open(out, "w") as f:
+        json.dump(d, f, indent=1)
+
+
 def main() -> None:
+    if len(sys.argv) == 4 and sys.argv[1] == "--recorrect":
+        return recorrect(sys.argv[2], sys.argv[3])
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
     ap.add_argument("--steps", type=int, default=3)
@@ -100,20 +126,18 @@ def main() -> None:
     result["bench_line"] = line
     nl = len(cfg["launches"])
     launch_bytes = [l.get("bytes") for l in cfg["launches"]]
-    wide = b.prec == 64
     out = {}
     for i in range(nl):
         f_kib = per_launch[i].get("FETCH_SIZE", 0.0)
         w_kib = per_launch[i].get("WRITE_SIZE", 0.0)
-        fetch = f_kib * 1024 * (2 if wide else 1)
+        fetch = f_kib * 1024 * 2
         write = w_kib * 1024
         out[str(i)] = fetch + write
         result["kernels"][str(i)] = {"kernel": per_launch[i]["kernel"], "FETCH_SIZE_KiB": f_kib,
                                      "WRITE_SIZE_KiB": w_kib, "fetch_bytes_corrected": fetch,
                                      "write_bytes": write, "algorithmic_bytes": launch_bytes[i]}
     result["per_launch_bytes"] = out
-    result["correction"] = ("FETCH_SIZE KiB x1024 x2 (gfx950 16 B/lane streaming read), WRITE_SIZE KiB x1024"
-                            if wide else "uncorrected (8 B/lane accesses uncalibrated)")
+    result["correction"] = correction(b.prec)
     # written under gpurun_out/ (merged back from the GPU box); copy into profiles/ to commit
     os.makedirs(args.outdir, exist_ok=True)
     path = os.path.join(args.outdir, f"{args.tag}_traffic_{key}.json")
