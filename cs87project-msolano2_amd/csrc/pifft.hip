@@ -525,16 +525,19 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             pc.vpt = 32;
         }
     }
-    // tuning: strided passes (and the fused tree pass) at PIFFT_STRIDED_VPT
-    // values per thread where that instance exists (8: radix-8 stages, twice
-    // the waves per workgroup)
+    // tuning: strided passes at PIFFT_STRIDED_VPT values per thread, the
+    // fused tree pass at PIFFT_FUSED_VPT, where that instance exists (8:
+    // radix-8 stages, twice the waves per workgroup)
     {
-        const int svpt = env_int("PIFFT_STRIDED_VPT", 0);
-        for (auto& pc : out)
-            if (svpt > 0 && (pc.mode == 1 || pc.mode == 2) &&
-                find_pass(prec, pc.R, pc.C, (pc.mode == 1 && heavy_lp) ? 3 : pc.mode, pc.nts,
-                          pc.mode == 1 ? heavy_lp : 0, svpt))
-                pc.vpt = svpt;
+        const int svpt = env_int("PIFFT_STRIDED_VPT", 0), fvpt = env_int("PIFFT_FUSED_VPT", 0);
+        for (size_t i = 0; i < out.size(); i++) {
+            PassChoice& pc = out[i];
+            const bool fused_pass = i == 0 && heavy_lp;
+            const int want = fused_pass ? fvpt : svpt;
+            if (want > 0 && (pc.mode == 1 || pc.mode == 2) &&
+                find_pass(prec, pc.R, pc.C, fused_pass ? 3 : pc.mode, pc.nts, fused_pass ? heavy_lp : 0, want))
+                pc.vpt = want;
+        }
     }
     // tuning: lines per workgroup of the last pass (its write side's segment width)
     const int last_c = env_int("PIFFT_LAST_C", 0);
@@ -607,6 +610,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
             const int cmin = env_int("PIFFT_WIL_CMIN", (int)p->P);
             if (cmin > pc.C && find_pass(p->prec, pc.R, cmin, pc.mode, pc.nts)) pc.C = cmin;
             ok = ok && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts) != nullptr;
+            const int wvpt = env_int("PIFFT_WIL_VPT", 0);  // tuning: values per thread
+            if (wvpt > 0 && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts, 0, wvpt)) pc.vpt = wvpt;
         }
         if (ok) {
             passes = w;

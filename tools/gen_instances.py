@@ -76,9 +76,21 @@ for R in (512, 1024):
 # per workgroup) for the latency-bound 2^20 configs: config 1's two 1024-point
 # passes at C = 4 and config 2's one-GPU slice (the fused tree + 512-point pass,
 # the 256-point pass), PIFFT_STRIDED_VPT=8 (tuning, round 4)
-for R, C, mode, lp in ((1024, 4, 1, 0), (1024, 4, 2, 0), (512, 4, 3, 3), (256, 4, 2, 0)):
+for R, C, mode, lp in ((1024, 4, 1, 0), (1024, 4, 2, 0), (256, 4, 2, 0)):
     for nts in (0, 1):
         items.append(f"PKV(double, 64, {R}, {C}, {mode}, {nts}, {lp}, 8),")
+# ... the fused tree pass at 8 values per thread for the small slices whose
+# fused launch has <= 128 workgroups (local 2^15-2^19: R = 256-1024 at C = 4),
+# both precisions, PIFFT_FUSED_VPT=8; and config 2's worker-interleaved passes
+# (C = 8), PIFFT_WIL_VPT=8 (tuning, round 4)
+for T, prec in (("double", 64), ("float", 32)):
+    for R in (256, 512, 1024):
+        for lp in (1, 2, 3, 4):
+            for nts in (0, 1):
+                items.append(f"PKV({T}, {prec}, {R}, 4, 3, {nts}, {lp}, 8),")
+for R in (256, 512):
+    for nts in (0, 1):
+        items.append(f"PKV(double, 64, {R}, 8, 10, {nts}, 0, 8),")
 # (a 32768-value tile -- C = 32 at R = 1024, one 1024-thread workgroup per CU,
 # 256-B segments -- made the fp32 2^28 last pass 0.88 -> 1.07 ms: round 4,
 # profiles/r04_fp32_last_pass_c32.log; not instantiated)
