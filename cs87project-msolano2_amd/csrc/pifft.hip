@@ -141,6 +141,7 @@ enum { BUF_IN = 0, BUF_OUT = 1, BUF_W = 2, BUF_TA = 3, NBUF = 4 };
 struct Step {
     int kind = 0;
     const void* fn = nullptr;
+    const PassKernel* pk = nullptr;  // STEP_PASS / STEP_TREE_PASS: the instance
     dim3 grid, block;
     size_t lds = 0;
     int src = -1, dst = -2;  // -1 / -2: the chain element's input / output buffer
@@ -786,6 +787,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
         s.fn = k->fn;
+        s.pk = k;
         s.nts = k->nts;
         const int logr = ilog2u((uint64_t)k->R);
         s.pa.tw_r = twp(tw_r[i]);
@@ -877,6 +879,30 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // at 1 GiB it ties, at 2 GiB (the worker of 2 at 2^28, of 8 at 2^30) it
     // gains ~0.5 % (profiles/r02_wpad.log, tools/gpu_wpad_shapes.sh).
     uint64_t w_tr = M;  // elements per transform in W
+    // tuning (PIFFT_W_BLOCK = log2 B): the blocked workspace between a MODE 2
+    // pass writing W and the MODE 2 pass reading it (PassArgs::blk): the
+    // reading pass's tiles of C <= B adjacent lines read one contiguous region
+    // instead of R rows 2^log_lb apart.  Such a pair is not padded.
+    const int w_blk = env_int("PIFFT_W_BLOCK", 0);
+    if (w_blk > 0 && !p->wil && !p->ilv) {
+        for (size_t i = 0; i + 1 < p->steps.size(); i++) {
+            Step& a = p->steps[i];
+            Step& b = p->steps[i + 1];
+            if (a.dst != BUF_W || b.src != BUF_W || a.kind != STEP_PASS || b.kind != STEP_PASS || !a.pk || !b.pk ||
+                a.pk->mode != 2 || b.pk->mode != 2 || (uint32_t)w_blk > b.pa.log_lb)
+                continue;
+            const PassKernel* ka = find_pass(p->prec, a.pk->R, a.pk->C, 2 | 32, a.pk->nts, 0, a.pk->vpt);
+            const PassKernel* kb = find_pass(p->prec, b.pk->R, b.pk->C, 2 | 16, b.pk->nts, 0, b.pk->vpt);
+            if (!ka || !kb) continue;
+            a.fn = ka->fn;
+            a.pk = ka;
+            b.fn = kb->fn;
+            b.pk = kb;
+            a.pa.blk = b.pa.blk = (uint32_t)w_blk;
+            a.pa.blk_l3 = b.pa.blk_l3 = b.pa.log_lb;
+            a.pa.blk_r = b.pa.blk_r = (uint32_t)ilog2u((uint64_t)kb->R);
+        }
+    }
     const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));
     const uint64_t w_min = (uint64_t)env_int("PIFFT_W_PAD_MIN_MIB", 2048) << 20;
     if (w_pad && !p->wil && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
@@ -884,7 +910,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
             if (a.dst != b.src || a.dst != BUF_W || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
-                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log)
+                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log || b.pa.blk)
                 continue;
             const uint64_t rows = M >> b.pa.log_lb;  // the reading pass's radix
             const uint64_t tr = M + rows * w_pad;

@@ -297,3 +297,30 @@ def test_position_model_orders_vs_oracle(logn, prec, P, monkeypatch):
             _check_bins(g, want, tol=tol)
     else:
         _check_bins(got["1"], got["0"], tol=tol)
+
+
+@pytest.mark.parametrize("prec", [pifft.F64, pifft.F32])
+def test_blocked_workspace_bitwise(prec, monkeypatch):
+    """The blocked workspace between the 2^28 plan's last two passes
+    (PassArgs::blk, PIFFT_W_BLOCK = log2 B, tuning): the same per-line
+    arithmetic on a permuted intermediate, so the output must equal the
+    default (padded-workspace) plan bit for bit, for B = 8, 16 and 32."""
+    n = 1 << 28
+    cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=cdt, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, prec, seed=33, stream=st)
+    base = pifft.Plan(n, 1, 1, prec)
+    ya = torch.empty_like(x)
+    base.execute_device(x.data_ptr(), ya.data_ptr(), st)
+    wb = base.describe()["workspace_bytes"]
+    base.close()
+    yb = torch.empty_like(x)
+    for blk in ("3", "4", "5"):
+        monkeypatch.setenv("PIFFT_W_BLOCK", blk)
+        plan = pifft.Plan(n, 1, 1, prec)
+        assert plan.describe()["workspace_bytes"] < wb  # (no row padding in the blocked pair)
+        plan.execute_device(x.data_ptr(), yb.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb)), blk
+        plan.close()

@@ -91,6 +91,12 @@ for T, prec in (("double", 64), ("float", 32)):
 for R in (256, 512):
     for nts in (0, 1):
         items.append(f"PKV(double, 64, {R}, 8, 10, {nts}, 0, 8),")
+# the blocked workspace between the last two passes of the 2^28 plans (MODE
+# 34 writes it, MODE 18 reads it; PassArgs::blk, PIFFT_W_BLOCK tuning, round 4)
+for R, C, mode in ((512, 16, 34), (1024, 8, 18)):
+    items.append(f"PK(double, 64, {R}, {C}, {mode}, 1, 0),")
+for R, C, mode in ((512, 32, 34), (1024, 16, 18)):
+    items.append(f"PKV(float, 32, {R}, {C}, {mode}, 1, 0, 32),")
 # (a 32768-value tile -- C = 32 at R = 1024, one 1024-thread workgroup per CU,
 # 256-B segments -- made the fp32 2^28 last pass 0.88 -> 1.07 ms: round 4,
 # profiles/r04_fp32_last_pass_c32.log; not instantiated)

@@ -17,3 +17,11 @@ cat "$out/fused_vpt8.log"
 timeout -k 10 120 python3 -u tools/tune.py --log-n 20 --prec 64 --workers 8 --steps 400 --warmup 20 --variants \
   '[{}, {"PIFFT_WIL_VPT": 8}, {}, {"PIFFT_WIL_VPT": 8}]' 2>&1 | grep -v "amdgpu.ids\|^torch" > "$out/wil_vpt8_c2.log" || exit 1
 cat "$out/wil_vpt8_c2.log"
+# the blocked workspace between the last two passes (PIFFT_W_BLOCK): bitwise tests, then timing
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py -k blocked -x -v --timeout 200 --timeout-method thread > "$out/blocked_tests.log" 2>&1 || { tail -30 "$out/blocked_tests.log"; exit 1; }
+tail -2 "$out/blocked_tests.log"
+for prec in 64 32; do
+  timeout -k 10 300 python3 -u tools/tune.py --log-n 28 --prec $prec --tune-ws 8 --steps 20 --variants \
+    '[{}, {"PIFFT_W_BLOCK": 4}, {"PIFFT_W_BLOCK": 3}, {"PIFFT_W_BLOCK": 5}, {}, {"PIFFT_W_BLOCK": 4}, {"PIFFT_W_BLOCK": 3}]' 2>&1 | grep -v "amdgpu.ids" > "$out/blocked_f$prec.log" || exit 1
+  cat "$out/blocked_f$prec.log"
+done
