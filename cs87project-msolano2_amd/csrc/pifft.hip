@@ -883,24 +883,29 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // pass writing W and the MODE 2 pass reading it (PassArgs::blk): the
     // reading pass's tiles of C <= B adjacent lines read one contiguous region
     // instead of R rows 2^log_lb apart.  Such a pair is not padded.
-    const int w_blk = env_int("PIFFT_W_BLOCK", 0);
-    if (w_blk > 0 && !p->wil && !p->ilv) {
+    // PIFFT_Y_BLOCK: the same for a hand-off through the caller's output (the
+    // first pass of a three-pass plan writes it, the second reads it; the last
+    // pass overwrites it with the result).
+    const int w_blk = env_int("PIFFT_W_BLOCK", 0), y_blk = env_int("PIFFT_Y_BLOCK", 0);
+    if ((w_blk > 0 || y_blk > 0) && !p->wil && !p->ilv) {
         for (size_t i = 0; i + 1 < p->steps.size(); i++) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
-            if (a.dst != BUF_W || b.src != BUF_W || a.kind != STEP_PASS || b.kind != STEP_PASS || !a.pk || !b.pk ||
-                a.pk->mode != 2 || b.pk->mode != 2 || (uint32_t)w_blk > b.pa.log_lb)
+            const int blk = a.dst == BUF_W ? w_blk : a.dst == BUF_OUT ? y_blk : 0;
+            if (blk <= 0 || a.dst != b.src || a.kind != STEP_PASS || b.kind != STEP_PASS || !a.pk || !b.pk ||
+                ((a.pk->mode & 3) != 1 && (a.pk->mode & 3) != 2) || (b.pk->mode & 3) != 2 ||
+                (uint32_t)blk > b.pa.log_lb || a.pa.blk_l3 /* a already writes blocked */)
                 continue;
-            const PassKernel* ka = find_pass(p->prec, a.pk->R, a.pk->C, 2 | 32, a.pk->nts, 0, a.pk->vpt);
-            const PassKernel* kb = find_pass(p->prec, b.pk->R, b.pk->C, 2 | 16, b.pk->nts, 0, b.pk->vpt);
-            if (!ka || !kb) continue;
+            const PassKernel* ka = find_pass(p->prec, a.pk->R, a.pk->C, a.pk->mode | 32, a.pk->nts, 0, a.pk->vpt);
+            const PassKernel* kb = find_pass(p->prec, b.pk->R, b.pk->C, b.pk->mode | 16, b.pk->nts, 0, b.pk->vpt);
+            if (!ka || !kb || (a.pa.blk && a.pa.blk != (uint32_t)blk)) continue;  // (one B per kernel)
             a.fn = ka->fn;
             a.pk = ka;
             b.fn = kb->fn;
             b.pk = kb;
-            a.pa.blk = b.pa.blk = (uint32_t)w_blk;
-            a.pa.blk_l3 = b.pa.blk_l3 = b.pa.log_lb;
-            a.pa.blk_r = b.pa.blk_r = (uint32_t)ilog2u((uint64_t)kb->R);
+            a.pa.blk = b.pa.blk = (uint32_t)blk;
+            a.pa.blk_l3 = b.pa.log_lb;
+            a.pa.blk_r = (uint32_t)ilog2u((uint64_t)kb->R);
         }
     }
     const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));

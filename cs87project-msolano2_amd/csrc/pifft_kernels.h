@@ -727,7 +727,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     constexpr bool BREV = (MODE & 4) != 0;
     constexpr bool WIL = (MODE & 8) != 0;  // worker-interleaved layout (PassArgs::wil)
     constexpr bool BLKIN = (MODE & 16) != 0, BLKOUT = (MODE & 32) != 0;  // blocked workspace (PassArgs::blk)
-    static_assert(!(BLKIN || BLKOUT) || (BM == 2 && !WIL && !BREV), "blocked workspace: later passes only");
+    static_assert(!BLKIN || BM == 2, "blocked reads: later passes only");
+    static_assert(!BLKOUT || ((BM == 1 || BM == 2) && !WIL && !BREV), "blocked writes: strided passes");
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
@@ -1076,7 +1077,7 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
     static_assert(BM == 1 || BM == 2, "packed VPT-32 passes: strided first / later passes");
     static_assert((MODE & ~(3 | 16 | 32)) == 0 && (NTS == 0 || NTS == 1), "no bit-reversed or interleaved forms");
     constexpr bool BLKIN = (MODE & 16) != 0, BLKOUT = (MODE & 32) != 0;  // blocked workspace (PassArgs::blk)
-    static_assert(!(BLKIN || BLKOUT) || BM == 2, "blocked workspace: later passes only");
+    static_assert(!BLKIN || BM == 2, "blocked reads: later passes only");
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
@@ -1276,7 +1277,8 @@ constexpr int pass_waves_per_eu() {
 // MODE 3: first pass with the tree stage fused in (one worker, P = 2^LP):
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
-// MODE 18 / 34: MODE 2 reading / writing the blocked workspace (PassArgs::blk)
+// MODE | 16 / MODE | 32: reading / writing the blocked intermediate (PassArgs::blk):
+//         18 and 34 (later passes), 33 (a first pass writing it), 50 (both)
 // NTS: non-temporal streaming of the data (nt_loads / nt_stores)
 template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16>
 __global__ __launch_bounds__((PassCfg<R, C, VPT>::NT), (pass_waves_per_eu<T, R, C, MODE, LP, VPT>()))

@@ -93,9 +93,11 @@ for R in (256, 512):
         items.append(f"PKV(double, 64, {R}, 8, 10, {nts}, 0, 8),")
 # the blocked workspace between the last two passes of the 2^28 plans (MODE
 # 34 writes it, MODE 18 reads it; PassArgs::blk, PIFFT_W_BLOCK tuning, round 4)
-for R, C, mode in ((512, 16, 34), (1024, 8, 18)):
+# (33: a first pass writing it, 50: a middle pass reading and writing it --
+# the hand-off through the caller's output, PIFFT_Y_BLOCK)
+for R, C, mode in ((512, 16, 34), (1024, 8, 18), (512, 16, 33), (512, 16, 50)):
     items.append(f"PK(double, 64, {R}, {C}, {mode}, 1, 0),")
-for R, C, mode in ((512, 32, 34), (1024, 16, 18)):
+for R, C, mode in ((512, 32, 34), (1024, 16, 18), (512, 32, 33), (512, 32, 50)):
     items.append(f"PKV(float, 32, {R}, {C}, {mode}, 1, 0, 32),")
 # (a 32768-value tile -- C = 32 at R = 1024, one 1024-thread workgroup per CU,
 # 256-B segments -- made the fp32 2^28 last pass 0.88 -> 1.07 ms: round 4,
