@@ -95,9 +95,11 @@ for R in (256, 512):
 # 34 writes it, MODE 18 reads it; PassArgs::blk, PIFFT_W_BLOCK tuning, round 4)
 # (33: a first pass writing it, 50: a middle pass reading and writing it --
 # the hand-off through the caller's output, PIFFT_Y_BLOCK)
-for R, C, mode in ((512, 16, 34), (1024, 8, 18), (512, 16, 33), (512, 16, 50)):
+# (and for the 512-1024-512 order with both hand-offs blocked: the 1024-point
+# pass in the middle (50), a 512-point last pass reading it (18))
+for R, C, mode in ((512, 16, 34), (1024, 8, 18), (512, 16, 33), (512, 16, 50), (1024, 8, 50), (512, 16, 18)):
     items.append(f"PK(double, 64, {R}, {C}, {mode}, 1, 0),")
-for R, C, mode in ((512, 32, 34), (1024, 16, 18), (512, 32, 33), (512, 32, 50)):
+for R, C, mode in ((512, 32, 34), (1024, 16, 18), (512, 32, 33), (512, 32, 50), (1024, 16, 50), (512, 32, 18)):
     items.append(f"PKV(float, 32, {R}, {C}, {mode}, 1, 0, 32),")
 # (a 32768-value tile -- C = 32 at R = 1024, one 1024-thread workgroup per CU,
 # 256-B segments -- made the fp32 2^28 last pass 0.88 -> 1.07 ms: round 4,

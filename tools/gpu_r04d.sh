@@ -22,6 +22,6 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py -k blocked -x -
 tail -2 "$out/blocked_tests.log"
 for prec in 64 32; do
   timeout -k 10 300 python3 -u tools/tune.py --log-n 28 --prec $prec --tune-ws 8 --steps 20 --variants \
-    '[{}, {"PIFFT_W_BLOCK": 4}, {"PIFFT_W_BLOCK": 3}, {"PIFFT_Y_BLOCK": 4}, {"PIFFT_W_BLOCK": 4, "PIFFT_Y_BLOCK": 4}, {}, {"PIFFT_W_BLOCK": 4}, {"PIFFT_W_BLOCK": 3}, {"PIFFT_Y_BLOCK": 4}, {"PIFFT_W_BLOCK": 4, "PIFFT_Y_BLOCK": 4}]' 2>&1 | grep -v "amdgpu.ids" > "$out/blocked_f$prec.log" || exit 1
+    '[{}, {"PIFFT_W_BLOCK": 4}, {"PIFFT_W_BLOCK": 3}, {"PIFFT_Y_BLOCK": 4}, {"PIFFT_W_BLOCK": 4, "PIFFT_Y_BLOCK": 4}, {}, {"PIFFT_W_BLOCK": 4}, {"PIFFT_W_BLOCK": 3}, {"PIFFT_Y_BLOCK": 4}, {"PIFFT_W_BLOCK": 4, "PIFFT_Y_BLOCK": 4}, {"PIFFT_RADIX_LOGS": "9,10,9", "PIFFT_W_BLOCK": 4, "PIFFT_Y_BLOCK": 4}, {"PIFFT_RADIX_LOGS": "9,10,9"}]' 2>&1 | grep -v "amdgpu.ids" > "$out/blocked_f$prec.log" || exit 1
   cat "$out/blocked_f$prec.log"
 done
