@@ -1370,6 +1370,7 @@ int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
         while (f < fns.size() && fns[f] != p->steps[i].fn) f++;
         if (f == fns.size()) fns.push_back(p->steps[i].fn);
         info->launch_fn[i] = (int32_t)f;
+        info->launch_mode[i] = p->steps[i].pk ? p->steps[i].pk->mode : 0;
     }
     return 0;
 }

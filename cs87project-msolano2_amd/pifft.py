@@ -53,6 +53,7 @@ class PlanInfo(ctypes.Structure):
         ("launch_kind", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("launch_fn", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("vpt", ctypes.c_int32 * 8),
+        ("launch_mode", ctypes.c_int32 * MAX_LAUNCH_INFO),
         ("layout", ctypes.c_int32),
     ]
 
@@ -255,6 +256,7 @@ def describe_info(i: PlanInfo) -> dict:
         "launch_bytes": list(i.launch_bytes[: min(nl, MAX_LAUNCH_INFO)]),
         "launch_kind": [KIND_NAMES.get(k, "?") for k in i.launch_kind[: min(nl, MAX_LAUNCH_INFO)]],
         "launch_fn": list(i.launch_fn[: min(nl, MAX_LAUNCH_INFO)]),
+        "launch_mode": list(i.launch_mode[: min(nl, MAX_LAUNCH_INFO)]),
         "vpt": list(i.vpt[: i.num_passes]),
         "worker_interleaved": bool(i.layout & 1), "natural_store": bool(i.layout & 2),
     }

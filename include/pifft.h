@@ -98,6 +98,10 @@ typedef struct pifft_plan_info {
                                   of first use) -- what rocprof aggregates per kernel */
     int32_t vpt[8];          /* complex values per thread of each pass (16; 32 for the
                                 packed fp32 passes of large transforms)            */
+    int32_t launch_mode[PIFFT_MAX_LAUNCH_INFO]; /* k_pass MODE of each pass launch (bits 0-1: single /
+                                  first / later / fused-tree pass, 4 bit-reversed store, 8
+                                  worker-interleaved, 16 / 32 reads / writes the blocked
+                                  intermediate); 0 for tree and interleave launches */
     int32_t layout;          /* bit 0: worker-interleaved passes (all P <= 16 workers of a
                                 natural-order plan: the last pass writes natural order);
                                 bit 1: the last pass stores natural order from the
