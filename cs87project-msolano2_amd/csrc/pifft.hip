@@ -526,19 +526,19 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
             pc.vpt = 32;
         }
     }
-    // tuning: strided passes at PIFFT_STRIDED_VPT values per thread, the
-    // fused tree pass at PIFFT_FUSED_VPT, where that instance exists (8:
-    // radix-8 stages, twice the waves per workgroup)
-    {
-        const int svpt = env_int("PIFFT_STRIDED_VPT", 0), fvpt = env_int("PIFFT_FUSED_VPT", 0);
-        for (size_t i = 0; i < out.size(); i++) {
-            PassChoice& pc = out[i];
-            const bool fused_pass = i == 0 && heavy_lp;
-            const int want = fused_pass ? fvpt : svpt;
-            if (want > 0 && (pc.mode == 1 || pc.mode == 2) &&
-                find_pass(prec, pc.R, pc.C, fused_pass ? 3 : pc.mode, pc.nts, fused_pass ? heavy_lp : 0, want))
-                pc.vpt = want;
-        }
+    // The fused tree pass of a small one-worker slice at 8 values per thread
+    // (radix-8 stages, twice the waves per workgroup) when it has R <= 512
+    // points and at most 128 workgroups: a latency-bound launch on a fraction
+    // of the CUs, whose P leaf loads and tree per value then spread over twice
+    // the threads.  Measured on MI355X (profiles/r04d_fused_vpt8.log): fp64
+    // local 2^15-2^18 +4.5-31 % (config 2's slice 14.05 -> 12.66 us), fp32
+    // +0.6-4 %; R = 1024 -2-3 %, 256 workgroups ties.  PIFFT_FUSED_VPT: the
+    // values per thread instead (tuning).
+    if (heavy_lp && !out.empty() && out[0].mode == 1) {
+        PassChoice& pc = out[0];
+        const uint64_t wgs = (ntrans * (M / (uint64_t)pc.R) + pc.C - 1) / (uint64_t)pc.C;
+        const int fvpt = env_int("PIFFT_FUSED_VPT", (pc.R <= 512 && wgs <= 128) ? 8 : 16);
+        if (fvpt != pc.vpt && find_pass(prec, pc.R, pc.C, 3, pc.nts, heavy_lp, fvpt)) pc.vpt = fvpt;
     }
     // tuning: lines per workgroup of the last pass (its write side's segment width)
     const int last_c = env_int("PIFFT_LAST_C", 0);
@@ -611,8 +611,12 @@ int build_plan(pifft_plan* p, bool dry = false) {
             const int cmin = env_int("PIFFT_WIL_CMIN", (int)p->P);
             if (cmin > pc.C && find_pass(p->prec, pc.R, cmin, pc.mode, pc.nts)) pc.C = cmin;
             ok = ok && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts) != nullptr;
-            const int wvpt = env_int("PIFFT_WIL_VPT", 0);  // tuning: values per thread
-            if (wvpt > 0 && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts, 0, wvpt)) pc.vpt = wvpt;
+            // config-2-sized plans (<= 32 MiB of data): 8 values per thread
+            // where instantiated (config 2 29.9 -> 29.0 us, profiles/
+            // r04d_wil_vpt8_c2.log); PIFFT_WIL_VPT: instead (tuning)
+            const bool small = (uint64_t)p->batch * p->n * esz <= (32ull << 20);
+            const int wvpt = env_int("PIFFT_WIL_VPT", small ? 8 : 16);
+            if (wvpt != pc.vpt && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts, 0, wvpt)) pc.vpt = wvpt;
         }
         if (ok) {
             passes = w;
@@ -879,35 +883,6 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // at 1 GiB it ties, at 2 GiB (the worker of 2 at 2^28, of 8 at 2^30) it
     // gains ~0.5 % (profiles/r02_wpad.log, tools/gpu_wpad_shapes.sh).
     uint64_t w_tr = M;  // elements per transform in W
-    // tuning (PIFFT_W_BLOCK = log2 B): the blocked workspace between a MODE 2
-    // pass writing W and the MODE 2 pass reading it (PassArgs::blk): the
-    // reading pass's tiles of C <= B adjacent lines read one contiguous region
-    // instead of R rows 2^log_lb apart.  Such a pair is not padded.
-    // PIFFT_Y_BLOCK: the same for a hand-off through the caller's output (the
-    // first pass of a three-pass plan writes it, the second reads it; the last
-    // pass overwrites it with the result).
-    const int w_blk = env_int("PIFFT_W_BLOCK", 0), y_blk = env_int("PIFFT_Y_BLOCK", 0);
-    if ((w_blk > 0 || y_blk > 0) && !p->wil && !p->ilv) {
-        for (size_t i = 0; i + 1 < p->steps.size(); i++) {
-            Step& a = p->steps[i];
-            Step& b = p->steps[i + 1];
-            const int blk = a.dst == BUF_W ? w_blk : a.dst == BUF_OUT ? y_blk : 0;
-            if (blk <= 0 || a.dst != b.src || a.kind != STEP_PASS || b.kind != STEP_PASS || !a.pk || !b.pk ||
-                ((a.pk->mode & 3) != 1 && (a.pk->mode & 3) != 2) || (b.pk->mode & 3) != 2 ||
-                (uint32_t)blk > b.pa.log_lb || a.pa.blk_l3 /* a already writes blocked */)
-                continue;
-            const PassKernel* ka = find_pass(p->prec, a.pk->R, a.pk->C, a.pk->mode | 32, a.pk->nts, 0, a.pk->vpt);
-            const PassKernel* kb = find_pass(p->prec, b.pk->R, b.pk->C, b.pk->mode | 16, b.pk->nts, 0, b.pk->vpt);
-            if (!ka || !kb || (a.pa.blk && a.pa.blk != (uint32_t)blk)) continue;  // (one B per kernel)
-            a.fn = ka->fn;
-            a.pk = ka;
-            b.fn = kb->fn;
-            b.pk = kb;
-            a.pa.blk = b.pa.blk = (uint32_t)blk;
-            a.pa.blk_l3 = b.pa.log_lb;
-            a.pa.blk_r = (uint32_t)ilog2u((uint64_t)kb->R);
-        }
-    }
     const uint64_t w_pad = (uint64_t)env_int("PIFFT_W_PAD", (int)((16384 + 256) / esz));
     const uint64_t w_min = (uint64_t)env_int("PIFFT_W_PAD_MIN_MIB", 2048) << 20;
     if (w_pad && !p->wil && (uint64_t)p->batch * p->nq * M * esz >= w_min) {
@@ -915,7 +890,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
             Step& a = p->steps[i];
             Step& b = p->steps[i + 1];
             if (a.dst != b.src || a.dst != BUF_W || (a.kind != STEP_PASS && a.kind != STEP_TREE_PASS) ||
-                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log || b.pa.blk)
+                b.kind != STEP_PASS || b.pa.log_ns == 0 || a.pa.ilv_log)
                 continue;
             const uint64_t rows = M >> b.pa.log_lb;  // the reading pass's radix
             const uint64_t tr = M + rows * w_pad;

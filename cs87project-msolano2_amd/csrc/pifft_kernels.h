@@ -458,14 +458,6 @@ struct PassArgs {
     // or slow (pass 3 1.58 vs 1.70-1.86 ms) by how the two allocations
     // happened to line up (tools/probe_place.py, tools/probe_pair.hip).
     uint32_t in_pad, out_pad, out_pad_log;
-    // Blocked workspace (MODE | 16 reads it, MODE | 32 writes it; round 4):
-    // the reading pass's element (j, r) -- its line j < 2^log_lb, radix index
-    // r -- sits at ((j >> blk) << (blk + log2 R)) + (r << blk) + (j & (2^blk - 1)),
-    // so a tile of C <= 2^blk adjacent lines reads one contiguous region of
-    // 2^blk R values instead of R rows 2^log_lb apart.  The writing pass maps
-    // its Stockham output e to (j, r) = (e mod 2^blk_l3, e >> blk_l3) of the
-    // reading pass (blk_l3 = that pass's log_lb, blk_r = its log2 R).
-    uint32_t blk, blk_l3, blk_r;
     // Worker-interleaved layout (MODE | 8, all P <= 16 workers of a natural-
     // order plan on one GPU): worker q's element e of transform bt sits at
     // bt bstride + e 2^wil + q, and launch line L = (j << wil) + q within a
@@ -726,9 +718,6 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     constexpr int BM = MODE & 3;
     constexpr bool BREV = (MODE & 4) != 0;
     constexpr bool WIL = (MODE & 8) != 0;  // worker-interleaved layout (PassArgs::wil)
-    constexpr bool BLKIN = (MODE & 16) != 0, BLKOUT = (MODE & 32) != 0;  // blocked workspace (PassArgs::blk)
-    static_assert(!BLKIN || BM == 2, "blocked reads: later passes only");
-    static_assert(!BLKOUT || ((BM == 1 || BM == 2) && !WIL && !BREV), "blocked writes: strided passes");
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
@@ -838,11 +827,9 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     __builtin_amdgcn_sched_barrier(0);  // next round's leaves after this one's trees
                 });
             } else if constexpr (BM == 2) {
-                // rows 2^les + in_pad apart (padded workspace, PassArgs::in_pad),
-                // or 2^blk apart in the blocked workspace (MODE | 16)
-                const uint64_t rs = BLKIN ? (1ull << a.blk) : (1ull << les) + a.in_pad;
-                const uint64_t jb = BLKIN ? ((j >> a.blk) << (a.blk + Sh::LOGR)) + (j & (rs - 1)) : j;
-                const C2* row = in + bin * a.in_bstride + jb + (uint64_t)b * rs;
+                // rows 2^les + in_pad apart (padded workspace, PassArgs::in_pad)
+                const uint64_t rs = (1ull << les) + a.in_pad;
+                const C2* row = in + bin * a.in_bstride + j + (uint64_t)b * rs;
 #pragma unroll
                 for (int k = 0; k < q; k++)
                     v[u * q + k] = ok ? ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs) : C2{(T)0, (T)0};
@@ -946,16 +933,6 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                     const uint32_t ks = lns + wil;
 #pragma unroll
                     for (int k = 0; k < q; k++) st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << ks), v[u * q + k]);
-                } else if constexpr (BLKOUT) {
-                    // the next pass's blocked layout (PassArgs::blk)
-                    C2* dst = out + bt * a.out_bstride;
-                    const uint64_t m3 = (1ull << a.blk_l3) - 1, mb = (1ull << a.blk) - 1;
-#pragma unroll
-                    for (int k = 0; k < q; k++) {
-                        const uint64_t e = pos + ((uint64_t)(k * NB) << lns), j3 = e & m3, r3 = e >> a.blk_l3;
-                        st_stream<nt_stores(NTS)>(dst + ((j3 >> a.blk) << (a.blk + a.blk_r)) + (r3 << a.blk) + (j3 & mb),
-                                                  v[u * q + k]);
-                    }
                 } else if constexpr (!BREV) {
                     // (ilv_log = 0: dst = out + bt out_bstride + pos + k NB 2^lns)
                     const uint32_t il = a.ilv_log;
@@ -1075,9 +1052,7 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
     constexpr int VPT = 32;
     constexpr int BM = MODE & 3;
     static_assert(BM == 1 || BM == 2, "packed VPT-32 passes: strided first / later passes");
-    static_assert((MODE & ~(3 | 16 | 32)) == 0 && (NTS == 0 || NTS == 1), "no bit-reversed or interleaved forms");
-    constexpr bool BLKIN = (MODE & 16) != 0, BLKOUT = (MODE & 32) != 0;  // blocked workspace (PassArgs::blk)
-    static_assert(!BLKIN || BM == 2, "blocked reads: later passes only");
+    static_assert((MODE & ~3) == 0 && (NTS == 0 || NTS == 1), "no bit-reversed or interleaved forms");
     using St = Stage<R, C, BM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
@@ -1116,9 +1091,8 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
             const uint64_t bt = line >> log_lb, j = line & lb_mask;
             const uint32_t les = log_lb;
             if constexpr (BM == 2) {
-                const uint64_t rs = BLKIN ? (1ull << a.blk) : (1ull << les) + a.in_pad;
-                const uint64_t jb = BLKIN ? ((j >> a.blk) << (a.blk + Sh::LOGR)) + (j & (rs - 1)) : j;
-                const C1* row = in + bt * a.in_bstride + jb + (uint64_t)b * rs;
+                const uint64_t rs = (1ull << les) + a.in_pad;
+                const C1* row = in + bt * a.in_bstride + j + (uint64_t)b * rs;
 #pragma unroll
                 for (int k = 0; k < q; k++)
                     pk_put<u & 1>(vp[(u >> 1) * q + k], ld_stream<nt_loads(NTS)>(row + (uint64_t)(k * NB) * rs));
@@ -1191,22 +1165,11 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
                 const uint64_t bt = line >> log_lb, j = line & lb_mask;
                 const uint32_t lns = (uint32_t)log_ns;
                 const uint64_t pos = ((j >> lns) << (lns + Sh::LOGR)) + (j & ((1ull << lns) - 1)) + ((uint64_t)b << lns);
-                if constexpr (BLKOUT) {
-                    C1* dst = out + bt * a.out_bstride;
-                    const uint64_t m3 = (1ull << a.blk_l3) - 1, mb = (1ull << a.blk) - 1;
+                const uint64_t pad = (j >> a.out_pad_log) * a.out_pad;
+                C1* dst = out + bt * a.out_bstride + pos + pad;
 #pragma unroll
-                    for (int k = 0; k < q; k++) {
-                        const uint64_t e = pos + ((uint64_t)(k * NB) << lns), j3 = e & m3, r3 = e >> a.blk_l3;
-                        st_stream<nt_stores(NTS)>(dst + ((j3 >> a.blk) << (a.blk + a.blk_r)) + (r3 << a.blk) + (j3 & mb),
-                                                  pk_get<u & 1>(vp[(u >> 1) * q + k]));
-                    }
-                } else {
-                    const uint64_t pad = (j >> a.out_pad_log) * a.out_pad;
-                    C1* dst = out + bt * a.out_bstride + pos + pad;
-#pragma unroll
-                    for (int k = 0; k < q; k++)
-                        st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << lns), pk_get<u & 1>(vp[(u >> 1) * q + k]));
-                }
+                for (int k = 0; k < q; k++)
+                    st_stream<nt_stores(NTS)>(dst + ((uint64_t)(k * NB) << lns), pk_get<u & 1>(vp[(u >> 1) * q + k]));
             }
         });
     } else {
@@ -1277,8 +1240,6 @@ constexpr int pass_waves_per_eu() {
 // MODE 3: first pass with the tree stage fused in (one worker, P = 2^LP):
 //         each input v_r = z_q[j + r M/R] is evaluated from its P leaves
 // MODE 4 / 6: MODE 0 / 2 storing in bit-reversed order (PIFFT_OUT_BITREV)
-// MODE | 16 / MODE | 32: reading / writing the blocked intermediate (PassArgs::blk):
-//         18 and 34 (later passes), 33 (a first pass writing it), 50 (both)
 // NTS: non-temporal streaming of the data (nt_loads / nt_stores)
 template <typename T, int R, int C, int MODE, int NTS, int LP, int VPT = 16>
 __global__ __launch_bounds__((PassCfg<R, C, VPT>::NT), (pass_waves_per_eu<T, R, C, MODE, LP, VPT>()))

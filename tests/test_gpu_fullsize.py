@@ -297,37 +297,3 @@ def test_position_model_orders_vs_oracle(logn, prec, P, monkeypatch):
             _check_bins(g, want, tol=tol)
     else:
         _check_bins(got["1"], got["0"], tol=tol)
-
-
-@pytest.mark.parametrize("prec", [pifft.F64, pifft.F32])
-def test_blocked_workspace_bitwise(prec, monkeypatch):
-    """The blocked intermediate layouts of the 2^28 plan (PassArgs::blk,
-    tuning): between the last two passes (PIFFT_W_BLOCK = log2 B, through the
-    workspace) and between the first two (PIFFT_Y_BLOCK, through the caller's
-    output).  The same per-line arithmetic on a permuted intermediate, so the
-    output equals the default plan's bit for bit, for B = 8, 16 and 32."""
-    n = 1 << 28
-    cdt = torch.complex128 if prec == pifft.F64 else torch.complex64
-    st = torch.cuda.current_stream()
-    x = torch.empty(n, dtype=cdt, device="cuda")
-    pifft.generate_device(x.data_ptr(), n, n, prec, seed=33, stream=st)
-    base = pifft.Plan(n, 1, 1, prec)
-    ya = torch.empty_like(x)
-    base.execute_device(x.data_ptr(), ya.data_ptr(), st)
-    wb = base.describe()["workspace_bytes"]
-    base.close()
-    yb = torch.empty_like(x)
-    for wblk, yblk in (("3", "0"), ("4", "0"), ("5", "0"), ("0", "4"), ("4", "4"), ("3", "3")):
-        monkeypatch.setenv("PIFFT_W_BLOCK", wblk)
-        monkeypatch.setenv("PIFFT_Y_BLOCK", yblk)
-        plan = pifft.Plan(n, 1, 1, prec)
-        if wblk != "0":
-            assert plan.describe()["workspace_bytes"] < wb  # (no row padding in the blocked pair)
-        names = [plan.kernel_name(i) for i in range(3)]
-        modes = [int(nm.split("<")[1].split(",")[3]) for nm in names]
-        assert modes == [1 | (32 if yblk != "0" else 0), 2 | (16 if yblk != "0" else 0) | (32 if wblk != "0" else 0),
-                         2 | (16 if wblk != "0" else 0)], names
-        plan.execute_device(x.data_ptr(), yb.data_ptr(), st)
-        torch.cuda.synchronize()
-        assert torch.equal(torch.view_as_real(ya), torch.view_as_real(yb)), (wblk, yblk)
-        plan.close()

@@ -718,8 +718,20 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
     x = oracle.generate(n * batch, DT[suf], seed=logn * 3 + P)
     d_in = dev(x)
     st = torch.cuda.current_stream()
+    # (the default plan, whose passes run at 8 values per thread at config-2
+    # sizes, against the oracle; then at 16, the slice-major plan's radices,
+    # value for value)
+    dflt = pifft.Plan(n, P, batch, PREC[suf])
+    a = torch.empty_like(d_in)
+    dflt.execute_device(d_in.data_ptr(), a.data_ptr(), st)
+    torch.cuda.synchronize()
+    got = a.cpu().numpy().reshape(batch, n)
+    for bt in range(batch):
+        assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
+    monkeypatch.setenv("PIFFT_WIL_VPT", "16")
     wil = pifft.Plan(n, P, batch, PREC[suf])
     assert wil.describe()["worker_interleaved"] and "interleave" not in wil.describe()["launch_kind"]
+    assert set(wil.describe()["vpt"]) == {16}
     monkeypatch.setenv("PIFFT_WORKER_IL", "0")
     sm = pifft.Plan(n, P, batch, PREC[suf])
     assert not sm.describe()["worker_interleaved"]

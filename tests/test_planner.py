@@ -250,3 +250,19 @@ def test_stray_tuning_variables_are_ignored(shape, monkeypatch):
     # ... and the same variables do take effect under PIFFT_TUNING=1
     monkeypatch.setenv("PIFFT_TUNING", "1")
     assert pifft.dry_run(n, P, b, prec, first=first, count=count, flags=flags) != want
+
+
+def test_small_slices_run_the_fused_pass_at_8_values_per_thread():
+    """Round 4 (profiles/r04d_fused_vpt8.log): a one-worker slice's fused tree
+    pass runs at 8 values per thread when it has R <= 512 points and at most
+    128 workgroups (config 2's slice: 14.05 -> 12.66 us); R = 1024 and larger
+    launches keep 16; config-2-sized worker-interleaved passes run at 8."""
+    d = pifft.dry_run(1 << 20, 8, 1, F64, first=0, count=1)   # config 2's slice: 512 x 256, 64 workgroups
+    assert d["launch_kind"][0] == "tree+pass" and d["radix"] == [512, 256] and d["vpt"] == [8, 16]
+    assert d["launch_mode"] == [3, 2]
+    assert pifft.dry_run(1 << 21, 8, 1, F64, first=7, count=1)["vpt"] == [8, 16]   # 128 workgroups
+    assert pifft.dry_run(1 << 20, 2, 1, F64, first=0, count=1)["vpt"] == [16, 16]  # R = 1024 first
+    assert pifft.dry_run(1 << 23, 8, 1, F64, first=0, count=1)["vpt"] == [16, 16]  # 256 workgroups
+    assert pifft.dry_run(1 << 28, 8, 1, F64, first=0, count=1)["vpt"] == [16, 16, 16]
+    assert pifft.dry_run(1 << 20, 8, 1, F64)["vpt"] == [8, 8]                     # config 2 (worker-interleaved)
+    assert pifft.dry_run(1 << 28, 8, 1, F64)["vpt"] == [16, 16, 16]

@@ -72,35 +72,26 @@ for R in (512, 1024):
     for nts in (0, 1):
         for mode in (1, 2):
             items.append(f"PKV(float, 32, {R}, {C}, {mode}, {nts}, 0, 32),")
-# fp64 strided passes at 8 values per thread (radix-8 stages, twice the waves
-# per workgroup) for the latency-bound 2^20 configs: config 1's two 1024-point
-# passes at C = 4 and config 2's one-GPU slice (the fused tree + 512-point pass,
-# the 256-point pass), PIFFT_STRIDED_VPT=8 (tuning, round 4)
-for R, C, mode, lp in ((1024, 4, 1, 0), (1024, 4, 2, 0), (256, 4, 2, 0)):
-    for nts in (0, 1):
-        items.append(f"PKV(double, 64, {R}, {C}, {mode}, {nts}, {lp}, 8),")
-# ... the fused tree pass at 8 values per thread for the small slices whose
-# fused launch has <= 128 workgroups (local 2^15-2^19: R = 256-1024 at C = 4),
-# both precisions, PIFFT_FUSED_VPT=8; and config 2's worker-interleaved passes
-# (C = 8), PIFFT_WIL_VPT=8 (tuning, round 4)
+# The fused tree pass at 8 values per thread (radix-8 stages, twice the waves
+# per workgroup) for small one-worker slices, whose fused launch has <= 128
+# workgroups (local 2^15-2^18: R = 256 / 512 at C = 4), both precisions; and
+# the worker-interleaved passes of config-2-sized all-worker plans (C = 8).
+# Measured on MI355X (profiles/r04d_fused_vpt8.log, r04d_wil_vpt8_c2.log):
+# fp64 slices +4.5-31 % (config 2's slice 14.05 -> 12.66 us), fp32 +0.6-4 %,
+# config 2 +4 %; R = 1024 fused passes -2-3 % and config 1's strided passes
+# -4 % at 8 (r04c_vpt8_c1.log): not instantiated.
 for T, prec in (("double", 64), ("float", 32)):
-    for R in (256, 512, 1024):
+    for R in (256, 512):
         for lp in (1, 2, 3, 4):
             for nts in (0, 1):
                 items.append(f"PKV({T}, {prec}, {R}, 4, 3, {nts}, {lp}, 8),")
 for R in (256, 512):
     for nts in (0, 1):
         items.append(f"PKV(double, 64, {R}, 8, 10, {nts}, 0, 8),")
-# the blocked workspace between the last two passes of the 2^28 plans (MODE
-# 34 writes it, MODE 18 reads it; PassArgs::blk, PIFFT_W_BLOCK tuning, round 4)
-# (33: a first pass writing it, 50: a middle pass reading and writing it --
-# the hand-off through the caller's output, PIFFT_Y_BLOCK)
-# (and for the 512-1024-512 order with both hand-offs blocked: the 1024-point
-# pass in the middle (50), a 512-point last pass reading it (18))
-for R, C, mode in ((512, 16, 34), (1024, 8, 18), (512, 16, 33), (512, 16, 50), (1024, 8, 50), (512, 16, 18)):
-    items.append(f"PK(double, 64, {R}, {C}, {mode}, 1, 0),")
-for R, C, mode in ((512, 32, 34), (1024, 16, 18), (512, 32, 33), (512, 32, 50), (1024, 16, 50), (512, 32, 18)):
-    items.append(f"PKV(float, 32, {R}, {C}, {mode}, 1, 0, 32),")
+# (blocked intermediates between the 2^28 passes -- the reading pass's tile a
+# contiguous region -- were built and lost 4-14 %: the writer's scattered
+# stores cost more than the reader gained; round 4,
+# profiles/r04d_blocked_intermediates.log; not instantiated)
 # (a 32768-value tile -- C = 32 at R = 1024, one 1024-thread workgroup per CU,
 # 256-B segments -- made the fp32 2^28 last pass 0.88 -> 1.07 ms: round 4,
 # profiles/r04_fp32_last_pass_c32.log; not instantiated)
