@@ -1228,9 +1228,13 @@ constexpr int first_tw_count() {
 
 // Workgroups per CU a k_pass instance is built for: two (PIFFT_MIN_WG_PER_CU),
 // one for the fused tree pass at P = 16 (its 16 leaves per input)
+#ifndef PIFFT_SINGLE_WPE
+#define PIFFT_SINGLE_WPE 0  // single passes of <= 256 threads: waves per SIMD to build for (0: the default rule)
+#endif
 template <typename T, int R, int C, int MODE, int LP, int VPT>
 constexpr int pass_waves_per_eu() {
     constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
+    if constexpr (PIFFT_SINGLE_WPE > 0 && (MODE & 3) == 0 && PassCfg<R, C, VPT>::NT <= 256) return PIFFT_SINGLE_WPE;
     return ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
 

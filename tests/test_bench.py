@@ -37,14 +37,20 @@ def _common(d, steps, warmup, n_gpus=1):
     assert abs(d["value"] - flops / (d["ms_per_step"] * 1e-3) / 1e9) <= tol
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
-    _roofline_ok(rf, d["ms_per_step"] if n_gpus == 1 else None)
+    _roofline_ok(rf, d["ms_per_step"] if n_gpus == 1 else None, contended=n_gpus > 1)
     assert len(d["config"]["launches"]) >= 1
 
 
-def _roofline_ok(rf, ms_per_step=None):
+def _roofline_ok(rf, ms_per_step=None, contended=False):
     """A roofline object is self-consistent: frac = achieved / peak, and the
     dominant kernel's (and all launches') time per step fits in the step of the
-    loop it was measured in (kernel-bound events; bench.py refuses otherwise)."""
+    loop it was measured in (kernel-bound events; bench.py refuses otherwise).
+    contended: a --same-device rehearsal rank, timed while 7 other ranks share
+    its GPU -- bench.py may refuse that frac (raw event times beyond the step);
+    the refusal is then all the object says."""
+    if contended and rf.get("frac") is None:
+        assert rf["error"].startswith("refused:") and rf["achieved"] is None, rf
+        return
     assert "error" not in rf, rf
     assert 0 < rf["achieved"] and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["algorithmic_bytes"] > 0
@@ -77,7 +83,7 @@ def test_bench_gpus_2_spawns_two_ranks():
     _common(d, 3, 1, n_gpus=2)
     pr = d["config"]["per_rank"]
     assert [r["rank"] for r in pr] == [0, 1] and [r["workers"] for r in pr] == [[0, 1], [1, 2]]
-    assert all(r["ms_per_step"] > 0 and 0 < r["frac"] for r in pr)
+    assert all(r["ms_per_step"] > 0 and (r["frac"] is None or 0 < r["frac"]) for r in pr)  # (None: refused, contended)
     # the job time is the slowest rank's
     assert d["ms_per_step"] >= max(r["ms_per_step"] for r in pr) * 0.999
     assert d["config"]["allgather_ms"] > 0
@@ -113,8 +119,8 @@ def test_bench_gpus_8_rehearsal_config5():
     assert sec["C5"]["allgather_ms"] > 0 and sec["C3_batch"]["batch_per_gpu"] == 512
     assert sec["C5"]["hbm_free_GiB"] >= sec["C5"]["hbm_need_GiB"]
     for key in ("C2_split", "C3_batch"):
-        _roofline_ok(sec[key]["roofline_rank0"])
-    _roofline_ok(sec["C5"]["roofline_rank0"])
+        _roofline_ok(sec[key]["roofline_rank0"], contended=True)
+    _roofline_ok(sec["C5"]["roofline_rank0"], contended=True)
     # self-verification of every worker split (round-3 verdict: the first 8-GPU run proves itself)
     v = d["config"]["verify"]
     assert v["ok"] and v["slices_bitwise"] and v["slices_checked"] == 8 and v["rel_l2"] <= 1e-12, v
