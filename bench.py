@@ -533,8 +533,8 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             flops = 5.0 * n * g["log_n"] * g["batch"]
             rf = job.roofline(ms)
             # PMC traffic of this very plan's dominant kernel, when a committed summary profiled it
-            key = f"n2^{g['log_n']}_f{32 if g['prec'] == F32 else 64}_b{g['batch']}_P{g['P']}_q{g['count']}"
-            rf["traffic"], rf["traffic_source"] = load_traffic(key, rf["launches"],
+            tkey = f"n2^{g['log_n']}_f{32 if g['prec'] == F32 else 64}_b{g['batch']}_P{g['P']}_q{g['count']}"
+            rf["traffic"], rf["traffic_source"] = load_traffic(tkey, rf["launches"],
                                                                [job.plan.kernel_name(i) for i in rf["launches"]])
             rec.update({"value": round(flops / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 6),
                         "steps": k, "dtype": "f64" if g["prec"] == F64 else "f32", "n": n, "workers": g["P"],

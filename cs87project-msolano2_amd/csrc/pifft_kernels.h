@@ -1228,13 +1228,12 @@ constexpr int first_tw_count() {
 
 // Workgroups per CU a k_pass instance is built for: two (PIFFT_MIN_WG_PER_CU),
 // one for the fused tree pass at P = 16 (its 16 leaves per input)
-#ifndef PIFFT_SINGLE_WPE
-#define PIFFT_SINGLE_WPE 0  // single passes of <= 256 threads: waves per SIMD to build for (0: the default rule)
-#endif
+// (config 3's single pass built for 8 waves per SIMD -- 64 VGPRs, 8 of its 16
+// workgroups per CU at once instead of 7 -- spills 18 B per lane and runs
+// 70 % slower: round 4, profiles/r04f_c3_wpe8.log)
 template <typename T, int R, int C, int MODE, int LP, int VPT>
 constexpr int pass_waves_per_eu() {
     constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
-    if constexpr (PIFFT_SINGLE_WPE > 0 && (MODE & 3) == 0 && PassCfg<R, C, VPT>::NT <= 256) return PIFFT_SINGLE_WPE;
     return ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
 
