@@ -1,6 +1,7 @@
 """Generates cs87project-msolano2_amd/csrc/pifft_instances_{0..NPART-1}.inc:
-the k_pass<T, R, C, MODE, NTS, LP> instantiations the planner may pick,
-spread over NPART translation units (compiled in parallel).
+the k_pass<T, R, C, MODE, NTS, LP, VPT> instantiations the planner may pick,
+spread over NPART translation units (compiled in parallel).  PK(...) is VPT 16;
+PKV(..., VPT) names the values per thread (8 or 32) explicitly.
 
 Rules: NT = C*R/VPT threads (VPT = 16 values per thread) <= 1024; LDS = C*(R + R/16 + 1)*sizeof(T)
 <= 160 KiB.  MODE 0 single pass (any C); MODE 1/2 strided passes (C >= 4);
