@@ -1385,6 +1385,35 @@ int pifft_execute_device(pifft_plan* p, const void* d_in, void* d_out, void* str
     return 0;
 }
 
+int pifft_launch_loop(pifft_plan* p, const int* launches, int nlaunches, int reps, const void* d_in, void* d_out,
+                      void* stream, float* mean_ms) {
+    if (check_buffers(p, d_in, d_out)) return -1;
+    if (!launches || nlaunches < 1 || reps < 1 || !mean_ms) return fail("bad arguments");
+    for (int j = 0; j < nlaunches; j++)
+        if (launches[j] < 0 || (size_t)launches[j] >= p->steps.size())
+            return fail("launch %d out of range (plan has %zu)", launches[j], p->steps.size());
+    DeviceGuard g(p->device);
+    hipStream_t st = (hipStream_t)stream;
+    auto rounds = [&](int r) -> int {
+        for (int k = 0; k < r; k++)
+            for (int j = 0; j < nlaunches; j++)
+                if (launch_step(p, p->steps[(size_t)launches[j]], d_in, d_out, st)) return -1;
+        return 0;
+    };
+    // the plan's own event pair, as markers around the loop (p->ev holds >= 2)
+    if (rounds(2)) return -1;
+    HIPCHK(hipEventRecord(p->ev[0], st));
+    if (rounds(reps)) return -1;
+    HIPCHK(hipEventRecord(p->ev[1], st));
+    if (launch_steps(p, d_in, d_out, st, nullptr)) return -1;  // d_out = the plan's result again
+    HIPCHK(hipEventSynchronize(p->ev[1]));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, p->ev[0], p->ev[1]));
+    HIPCHK(hipStreamSynchronize(st));
+    *mean_ms = ms / (float)((size_t)reps * (size_t)nlaunches);
+    return 0;
+}
+
 int pifft_plan_tune_workspace(pifft_plan* p, const void* d_in, void* d_out, void* stream, int tries,
                               float* best_ms) {
     if (check_buffers(p, d_in, d_out)) return -1;

@@ -92,6 +92,8 @@ _SIGS = {
     "pifft_plan_tune_workspace": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     "pifft_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int),
                                           ctypes.c_int]),
+    "pifft_launch_loop": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int, _P, _P, _P,
+                                         ctypes.POINTER(ctypes.c_float)]),
     "pifft_allgather": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_P),
                                        ctypes.POINTER(ctypes.c_double)]),
 }
@@ -221,6 +223,15 @@ class Plan:
         if used < 0:
             raise PifftError(f"pifft_profile_read: {last_error()}")
         return used, list(buf[:n]), list(cnt[:n])
+
+    def launch_loop(self, launches, reps: int, d_in: int, d_out: int, stream=None) -> float:
+        """pifft_launch_loop: mean ms of the given launches run alone, back to
+        back, `reps` rounds (d_out holds the plan's result afterwards)."""
+        ls = (ctypes.c_int * len(launches))(*launches)
+        ms = ctypes.c_float()
+        _check(lib().pifft_launch_loop(self._h, ls, len(launches), reps, d_in, d_out, _stream(stream),
+                                       ctypes.byref(ms)), "pifft_launch_loop")
+        return ms.value
 
     def execute(self, host_in, host_out=None):
         """numpy in -> natural-order numpy out (only this plan's bins written)."""

@@ -199,6 +199,17 @@ int pifft_plan_tune_workspace(pifft_plan* plan, const void* d_in, void* d_out, v
 int pifft_profile_start(pifft_plan* plan, int steps, int mode);
 int pifft_profile_read(pifft_plan* plan, float* launch_ms_sum, int* launch_samples, int max_launches);
 
+/* A clean loop of some of the plan's launches alone (profiling): after two
+ * untimed rounds, `reps` rounds of launches[0 .. nlaunches) back to back
+ * between two marker events, then one full execution, so d_out again holds
+ * the plan's result.  *mean_ms = the loop's time / (reps * nlaunches): a
+ * launch's duration back to back with itself plus its share of the dispatch
+ * gaps -- the timed loop's context without bound events, each of which lets
+ * the GPU idle ~9 us after its dispatch (a 10-us kernel sampled that way
+ * reads 5-8 % faster than back to back; round-4 trace).  Synchronous. */
+int pifft_launch_loop(pifft_plan* plan, const int* launches, int nlaunches, int reps, const void* d_in,
+                      void* d_out, void* stream, float* mean_ms);
+
 /* Host boundary, the reference's run() shape: copies host_in (batch*N values)
  * to the device (untimed), runs, and if host_out != NULL writes this plan's
  * bins at their natural-order positions of host_out (batch*N values; other

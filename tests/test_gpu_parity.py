@@ -322,6 +322,30 @@ def test_timed_execution_reports_every_launch():
     assert torch.equal(y, want)
 
 
+def test_launch_loop_times_and_restores_the_result():
+    """pifft_launch_loop (bench.py's dominant-kernel timing): a clean loop of
+    some launches alone, then one full execution -- the output is bitwise the
+    plan's result again (the loop re-runs launches on whatever their buffers
+    hold); out-of-range launches, reps < 1 and an empty list are refused."""
+    n = 1 << 20
+    plan = pifft.Plan(n, 8, 1, pifft.F64)
+    st = torch.cuda.current_stream()
+    x = torch.empty(n, dtype=torch.complex128, device="cuda")
+    pifft.generate_device(x.data_ptr(), n, n, pifft.F64, stream=st)
+    want = torch.empty(n, dtype=torch.complex128, device="cuda")
+    plan.execute_device(x.data_ptr(), want.data_ptr(), st)
+    y = torch.zeros_like(want)
+    nl = plan.info.num_launches
+    for ls in ([nl - 1], list(range(nl))):
+        ms = plan.launch_loop(ls, 50, x.data_ptr(), y.data_ptr(), st)
+        assert 0 < ms < 1.0, ms
+        torch.cuda.synchronize()
+        assert torch.equal(y, want)
+    for ls, reps in (([nl], 5), ([-1], 5), ([0], 0), ([], 5)):
+        with pytest.raises(pifft.PifftError):
+            plan.launch_loop(ls, reps, x.data_ptr(), y.data_ptr(), st)
+
+
 @pytest.mark.parametrize("suf,logn,P", [("f64", 22, 1), ("f32", 24, 1), ("f64", 21, 8)])
 def test_tune_workspace_keeps_results(suf, logn, P):
     """pifft_plan_tune_workspace only re-places the plan's workspace: the

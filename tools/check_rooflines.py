@@ -1,17 +1,26 @@
 #!/usr/bin/env python3
 """tools/check_rooflines.py <bench.json> <rocpd2summary dir> <rocpd .db> --
 checks every roofline of a bench line against rocprofv3 --kernel-trace of the
-same bench command in the same session (tools/gpu_r03.sh).
+same bench command in the same session (tools/gpu_r04.sh).
 
 The traced run executes the configs in bench.py's order (headline, then the
 secondary configs).  Dispatches are split into one cluster per config at each
-input generation (k_generate: every config's Job starts with one; its warm-up,
-timed and clean loops follow).  For each roofline the dominant kernel (by the
-demangled name bench.py records, pifft_plan_kernel_name) is averaged over its
-cluster's back-to-back dispatches (those starting within BACK_TO_BACK_US of the
-previous dispatch's end: the timed loop's context) and over all dispatches of
-that name (what --stats prints); the bench line's mean launch time is compared
-with the first.
+input generation (k_generate: every config's Job starts with one; its
+workspace tuning, warm-up, timed loop, profiling loop and the dominant
+kernel's clean loop follow).
+
+Lines that record trace_loop_dispatches (round 4 on: the dominant kernel
+timed as a clean loop of its launches, pifft_launch_loop) are checked like
+for like: the cluster's dispatches of that kernel are cut to the loop's timed
+rounds (the last trace_loop_dispatches before the one full execution that
+ends the loop), and the trace's figure is the loop's span (first start to
+last end) per dispatch -- the quantity the line's marker events measure; the
+mean kernel duration inside the loop (dispatch gaps excluded, what --stats
+averages) is printed beside it.
+
+Older lines (the dominant kernel from events bound to sampled dispatches)
+are compared with the mean duration of the cluster's back-to-back dispatches
+(those starting within BACK_TO_BACK_US of the previous dispatch's end).
 Done when every frac is within 3 % of rocprof's."""
 import csv
 import glob
@@ -35,6 +44,23 @@ def rooflines(line):
     return out
 
 
+def trace_figure(rf, cluster, name):
+    """(ms the line's figure is checked against, mean kernel ms, dispatches, how)."""
+    mine = [(s, e) for n, s, e, gap in cluster if n == name]
+    loop = int(rf.get("trace_loop_dispatches") or 0)
+    tail = len(rf.get("launches") or [])  # the full execution after the loop
+    if loop and loop + tail <= len(mine):
+        sel = mine[len(mine) - tail - loop:len(mine) - tail]
+        span = (sel[-1][1] - sel[0][0]) * 1e-6 / len(sel)
+        mean = sum(e - s for s, e in sel) * 1e-6 / len(sel)
+        return span, mean, len(sel), "loop span"
+    durs = [(e - s) * 1e-6 for (n, s, e, gap) in cluster if n == name and gap < BACK_TO_BACK_US]
+    if not durs:
+        return None, None, 0, ""
+    mean = sum(durs) / len(durs)
+    return mean, mean, len(durs), "back-to-back mean"
+
+
 def main():
     line = json.loads(open(sys.argv[1]).read().strip().splitlines()[0])
     stats = {}
@@ -50,25 +76,22 @@ def main():
         if "k_generate" in n:  # every config (bench.py Job) starts by generating its input
             clusters.append([])
         elif clusters:
-            clusters[-1].append((n, (e - s) * 1e-6, gap))
+            clusters[-1].append((n, s, e, gap))
     rfs = rooflines(line)
     print(f"{len(clusters)} dispatch clusters in the trace, {len(rfs)} rooflines in the line")
     worst, ok = 0.0, True
-    print(f"{'config':10s} {'bench ms':>10s} {'trace ms':>10s} {'stats ms':>10s} {'frac':>7s} {'frac(tr)':>8s} "
-          f"{'diff':>7s}  kernel")
+    print(f"{'config':10s} {'bench ms':>10s} {'trace ms':>10s} {'kern ms':>10s} {'stats ms':>10s} {'frac':>7s} "
+          f"{'frac(tr)':>8s} {'diff':>7s}  kernel")
     for i, (key, rf, step_ms) in enumerate(rfs):
         name = rf.get("kernel_name")
         if rf.get("frac") is None or not name:
             print(f"{key:10s} no frac in the line: {rf.get('error', 'no kernel name')}")
             ok = False
             continue
-        cl = clusters[i] if i < len(clusters) else []
-        # back-to-back dispatches only (the timed loop's context; a dispatch
-        # after one with bound events starts ~9 us late, isolated)
-        durs = [d for n, d, gap in cl if n == name and gap < BACK_TO_BACK_US]
-        tr = sum(durs) / len(durs) if durs else None
+        ref, kern, count, how = trace_figure(rf, clusters[i] if i < len(clusters) else [], name)
         st = stats.get(name, (0, None))[1]
-        ref = tr if tr is not None else st
+        if ref is None:
+            ref, kern, how = st, st, "--stats average"
         if ref is None:
             print(f"{key:10s} kernel not in the trace: {name}")
             ok = False
@@ -77,8 +100,9 @@ def main():
         diff = rf["frac"] / frac_tr - 1.0
         worst = max(worst, abs(diff))
         ok = ok and abs(diff) <= TOL
-        print(f"{key:10s} {rf.get('mean_ms', rf['algorithmic_bytes'] / (rf['achieved'] * 1e9) * 1e3):10.5f} {ref:10.5f} {st if st is not None else float('nan'):10.5f} "
-              f"{rf['frac']:7.4f} {frac_tr:8.4f} {diff:+7.2%}  {name}  ({len(durs)} dispatches)")
+        bench_ms = rf.get("mean_ms", rf["algorithmic_bytes"] / (rf["achieved"] * 1e9) * 1e3)
+        print(f"{key:10s} {bench_ms:10.5f} {ref:10.5f} {kern:10.5f} {st if st is not None else float('nan'):10.5f} "
+              f"{rf['frac']:7.4f} {frac_tr:8.4f} {diff:+7.2%}  {name}  ({count} dispatches, {how})")
     print(f"worst |frac difference| {worst:.2%}: {'OK' if ok else 'FAIL'} (tolerance {TOL:.0%})")
     return 0 if ok else 1
 
