@@ -940,7 +940,8 @@ def main() -> int:
     flops = 5.0 * n * args.log_n * args.batch  # the whole job's batch (every rank's share)
     value = flops / (ms_per_step * 1e-3) / 1e9
     if rank == 0:
-        rf_line = {k: rf[k] for k in ("bound", "kernel", "kernel_name", "mean_ms", "achieved", "peak", "unit", "frac")}
+        rf_line = {k: rf[k] for k in ("bound", "kernel", "kernel_name", "launches", "mean_ms", "loop_reps",
+                                      "trace_loop_dispatches", "sampled_mean_ms", "achieved", "peak", "unit", "frac")}
         rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"],
                         "kernel_ms_per_step": rf["kernel_ms_per_step"],
                         "all_launches_ms_per_step": rf["all_launches_ms_per_step"], "step_ms": rf["step_ms"],
