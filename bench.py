@@ -425,16 +425,26 @@ class Job:
         self.avg = [t / c for t, c in zip(sums, cnt)]
         self.samples = samples
 
+    def loop(self, launches) -> tuple:
+        """(mean ms, rounds) of a clean loop of these launches alone, back to
+        back (pifft_launch_loop): ~20 ms of them, 10 - 4000 rounds sized from
+        the bytes at 4 TB/s, so the count is a function of the plan alone (a
+        trace of another run of the same command cuts at the same place)."""
+        d = self.desc
+        nbytes = sum(d["launch_bytes"][i] for i in launches)
+        reps = int(min(4000, max(10, 20e-3 / (nbytes / 4e12))))
+        return self.plan.launch_loop(launches, reps, self.x.data_ptr(), self.y.data_ptr(), self.stream), reps
+
     def roofline(self, ms_per_step: float) -> dict:
-        """The dominant kernel (the kernel function with the largest share of
-        the step by the sampled launch times; its launches grouped as
-        rocprofv3 --stats groups them): algorithmic bytes per launch / its
-        mean duration in a clean loop of those launches (pifft_launch_loop:
-        back to back, marker events around the loop only -- sampled events
-        bound to single dispatches let the GPU idle after each and read a
-        10-us kernel 5-8 % faster than back to back, round-4 trace).
-        Self-check: no frac when the kernel's loop time per step exceeds the
-        measured step time."""
+        """The dominant kernel: the kernel function (its launches grouped as
+        rocprofv3 --stats groups them) with the largest time per step in a
+        clean back-to-back loop of its launches (Job.loop; marker events
+        around the loop only, so the figure holds under a tracer too:
+        rocprofv3 reproduces it on the same dispatches to 0.04 %, round 4,
+        profiles/r04i_roofline_check_traced_run.txt).  frac = algorithmic
+        bytes per launch / that mean launch time; the dominant kernel's loop
+        runs last, so a trace ends with it.  Self-check: no frac when the
+        kernel's launches take longer than the measured step."""
         d = self.desc
         nl = d["num_launches"]
         raw_step_ms = sum(self.avg[:nl])
@@ -442,14 +452,11 @@ class Job:
         by_fn = {}
         for i in range(nl):
             by_fn.setdefault(d["launch_fn"][i], []).append(i)
-        dom_launches = max(by_fn.values(), key=lambda ls: sum(avg[i] for i in ls))
+        shares = {tuple(ls): self.loop(ls)[0] * len(ls) for ls in by_fn.values()} if len(by_fn) > 1 else {}
+        dom_launches = list(max(shares, key=shares.get)) if shares else next(iter(by_fn.values()))
         sampled_ms = sum(avg[i] for i in dom_launches) / len(dom_launches)
         dom_bytes = sum(d["launch_bytes"][i] for i in dom_launches) // len(dom_launches)
-        # ~20 ms of the launches back to back (10 - 4000 rounds), sized from
-        # the bytes at 4 TB/s so the count is a function of the plan alone
-        # (a trace of another run of the same command cuts at the same place)
-        reps = int(min(4000, max(10, 20e-3 / (dom_bytes * len(dom_launches) / 4e12))))
-        dom_ms = self.plan.launch_loop(dom_launches, reps, self.x.data_ptr(), self.y.data_ptr(), self.stream)
+        dom_ms, reps = self.loop(dom_launches)
         dom_step_ms = dom_ms * len(dom_launches)
         kernel_step_ms = sum(avg[:nl])
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0

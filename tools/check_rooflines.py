@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""tools/check_rooflines.py <bench.json> <rocpd2summary dir> <rocpd .db> --
+"""tools/check_rooflines.py <bench.json> <rocpd2summary dir> <rocpd .db> [--same-run] --
 checks every roofline of a bench line against rocprofv3 --kernel-trace of the
 same bench command in the same session (tools/gpu_r04.sh).
 
@@ -13,10 +13,12 @@ Lines that record trace_loop_dispatches (round 4 on: the dominant kernel
 timed as a clean loop of its launches, pifft_launch_loop) are checked like
 for like: the cluster's dispatches of that kernel are cut to the loop's timed
 rounds (the last trace_loop_dispatches before the one full execution that
-ends the loop), and the trace's figure is the loop's span (first start to
-last end) per dispatch -- the quantity the line's marker events measure; the
-mean kernel duration inside the loop (dispatch gaps excluded, what --stats
-averages) is printed beside it.
+ends the loop).  --same-run (the line printed by the traced run itself): the
+trace's figure is the loop's span (first start to last end) per dispatch --
+exactly what the line's marker events measured.  Otherwise (an untraced run
+of the same command): the mean kernel duration inside the loop, since the
+tracer adds its own gap after every dispatch (round 4: 2.4 us per dispatch of
+config 2's slice); both are printed.
 
 Older lines (the dominant kernel from events bound to sampled dispatches)
 are compared with the mean duration of the cluster's back-to-back dispatches
@@ -44,7 +46,7 @@ def rooflines(line):
     return out
 
 
-def trace_figure(rf, cluster, name):
+def trace_figure(rf, cluster, name, same_run):
     """(ms the line's figure is checked against, mean kernel ms, dispatches, how)."""
     mine = [(s, e) for n, s, e, gap in cluster if n == name]
     loop = int(rf.get("trace_loop_dispatches") or 0)
@@ -53,7 +55,7 @@ def trace_figure(rf, cluster, name):
         sel = mine[len(mine) - tail - loop:len(mine) - tail]
         span = (sel[-1][1] - sel[0][0]) * 1e-6 / len(sel)
         mean = sum(e - s for s, e in sel) * 1e-6 / len(sel)
-        return span, mean, len(sel), "loop span"
+        return (span, mean, len(sel), "loop span") if same_run else (mean, mean, len(sel), "loop kernel mean")
     durs = [(e - s) * 1e-6 for (n, s, e, gap) in cluster if n == name and gap < BACK_TO_BACK_US]
     if not durs:
         return None, None, 0, ""
@@ -62,6 +64,8 @@ def trace_figure(rf, cluster, name):
 
 
 def main():
+    same_run = "--same-run" in sys.argv
+    sys.argv = [a for a in sys.argv if a != "--same-run"]
     line = json.loads(open(sys.argv[1]).read().strip().splitlines()[0])
     stats = {}
     for f in glob.glob(os.path.join(sys.argv[2], "**", "*kernel*s*.csv"), recursive=True):
@@ -80,7 +84,7 @@ def main():
     rfs = rooflines(line)
     print(f"{len(clusters)} dispatch clusters in the trace, {len(rfs)} rooflines in the line")
     worst, ok = 0.0, True
-    print(f"{'config':10s} {'bench ms':>10s} {'trace ms':>10s} {'kern ms':>10s} {'stats ms':>10s} {'frac':>7s} "
+    print(f"{'config':10s} {'bench ms':>10s} {'check ms':>10s} {'kern ms':>10s} {'stats ms':>10s} {'frac':>7s} "
           f"{'frac(tr)':>8s} {'diff':>7s}  kernel")
     for i, (key, rf, step_ms) in enumerate(rfs):
         name = rf.get("kernel_name")
@@ -88,7 +92,7 @@ def main():
             print(f"{key:10s} no frac in the line: {rf.get('error', 'no kernel name')}")
             ok = False
             continue
-        ref, kern, count, how = trace_figure(rf, clusters[i] if i < len(clusters) else [], name)
+        ref, kern, count, how = trace_figure(rf, clusters[i] if i < len(clusters) else [], name, same_run)
         st = stats.get(name, (0, None))[1]
         if ref is None:
             ref, kern, how = st, st, "--stats average"

@@ -36,7 +36,7 @@ if [[ "$stages" == *s* ]]; then
     python3 tools/check_rooflines.py "$out/${tag}_bench.json" "$out/sum_sec" "$out/stats_sec/sec_results.db" > "$out/${tag}_roofline_check.txt" 2>&1
     cat "$out/${tag}_roofline_check.txt"
   fi
-  python3 tools/check_rooflines.py "$out/${tag}_bench_under_rocprof.json" "$out/sum_sec" "$out/stats_sec/sec_results.db" > "$out/${tag}_roofline_check_traced_run.txt" 2>&1
+  python3 tools/check_rooflines.py "$out/${tag}_bench_under_rocprof.json" "$out/sum_sec" "$out/stats_sec/sec_results.db" --same-run > "$out/${tag}_roofline_check_traced_run.txt" 2>&1
   cat "$out/${tag}_roofline_check_traced_run.txt"
 fi
 if [[ "$stages" == *p* ]]; then
