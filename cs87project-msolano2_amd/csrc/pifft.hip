@@ -172,6 +172,9 @@ struct pifft_plan {
     bool fused_tree = false;  // tree evaluated inside the first pass (STEP_TREE_PASS)
     std::vector<Step> tree_only;  // the tree stage alone, for pifft_tree_device
     std::vector<hipEvent_t> prof_ev;  // pifft_profile_*: per recorded execution, a start and a stop per timed launch
+#ifdef PIFFT_WG_CLOCK
+    unsigned long long* dbg_clk = nullptr;  // pifft_debug_wg_clock: the clocked launch's words (diagnostics build)
+#endif
     int prof_steps = 0, prof_used = 0, prof_mode = 0;
     int radix[8] = {0}, lines[8] = {0}, vpt[8] = {0};
     void* buf[NBUF] = {nullptr};
@@ -989,6 +992,9 @@ int launch_step(pifft_plan* p, const Step& s, const void* d_in, void* d_out, hip
             PassArgs a = s.pa;
             a.in = src;
             a.out = dst;
+#ifdef PIFFT_WG_CLOCK
+            a.wg_clock = p->dbg_clk;
+#endif
             void* args[] = {&a};
             e = go(args, s.lds);
             break;
@@ -1413,6 +1419,46 @@ int pifft_launch_loop(pifft_plan* p, const int* launches, int nlaunches, int rep
     *mean_ms = ms / (float)((size_t)reps * (size_t)nlaunches);
     return 0;
 }
+
+#ifdef PIFFT_WG_CLOCK
+// Diagnostics build only (-DPIFFT_WG_CLOCK, tools/wg_clock.py; not in
+// include/pifft.h): `warm` full executions, then launches 0 .. launch-1 as
+// usual and `launch` with every workgroup recording its entry and
+// stores-done wall clock and hardware id (3 words per workgroup) into
+// host[0 .. min(3 grid, max_words)).  Returns the workgroup count (or -1);
+// *wall_hz = the wall clock's rate.  Synchronous.
+int pifft_debug_wg_clock(pifft_plan* p, int launch, const void* d_in, void* d_out, void* stream, int warm,
+                         unsigned long long* host, size_t max_words, unsigned long long* wall_hz) {
+    if (check_buffers(p, d_in, d_out)) return -1;
+    if (launch < 0 || (size_t)launch >= p->steps.size()) return fail("launch %d out of range", launch);
+    const Step& s = p->steps[(size_t)launch];
+    if (s.kind != STEP_PASS && s.kind != STEP_TREE_PASS) return fail("launch %d is not a pass", launch);
+    DeviceGuard g(p->device);
+    hipStream_t st = (hipStream_t)stream;
+    const size_t nwg = (size_t)s.grid.x * s.grid.y * s.grid.z, words = 3 * nwg;
+    unsigned long long* clk = nullptr;
+    HIPCHK(hipMalloc(&clk, words * sizeof(unsigned long long)));
+    int rc = 0;
+    for (int k = 0; k < warm && rc == 0; k++) rc = launch_steps(p, d_in, d_out, st, nullptr);
+    for (int i = 0; i < launch && rc == 0; i++) rc = launch_step(p, p->steps[(size_t)i], d_in, d_out, st);
+    if (rc == 0) {
+        p->dbg_clk = clk;
+        rc = launch_step(p, s, d_in, d_out, st);
+        p->dbg_clk = nullptr;
+    }
+    if (rc == 0 && hipStreamSynchronize(st) != hipSuccess) rc = fail("hipStreamSynchronize failed");
+    if (rc == 0 && hipMemcpy(host, clk, std::min(words, max_words) * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail("hipMemcpy failed");
+    int khz = 0;
+    if (rc == 0 && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device) != hipSuccess)
+        rc = fail("no wall clock rate");
+    (void)hipFree(clk);
+    if (rc) return -1;
+    *wall_hz = (unsigned long long)khz * 1000ull;
+    return (int)nwg;
+}
+#endif
 
 int pifft_plan_tune_workspace(pifft_plan* p, const void* d_in, void* d_out, void* stream, int tries,
                               float* best_ms) {

@@ -467,6 +467,11 @@ struct PassArgs {
     // natural-order result bitrev(q) + P k directly: no interleave launch and
     // no scattered 16-B stores.
     uint32_t wil, wbrev;
+#ifdef PIFFT_WG_CLOCK
+    // diagnostics build only (tools/wg_clock.py): 3 words per workgroup --
+    // wall clock at entry, wall clock once its stores completed, hardware id
+    unsigned long long* wg_clock;
+#endif
 };
 
 __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, uint32_t nblocks) {
@@ -1257,6 +1262,9 @@ void k_pass(PassArgs a) {
     uint64_t tile = tile_of_block(blockIdx.x, a.log_xg, gridDim.x);
     T* lds = reinterpret_cast<T*>(pifft_smem);
     const int tid = (int)threadIdx.x;
+#ifdef PIFFT_WG_CLOCK
+    if (a.wg_clock && tid == 0) a.wg_clock[3 * blockIdx.x] = wall_clock64();
+#endif
     if constexpr (VPT == 32 && std::is_same_v<T, float> && PIFFT_PACK32) {
         cx<f2> vp[PassShape<R, VPT>::Q / 2];
         cx<float> twp[TWN];
@@ -1276,6 +1284,16 @@ void k_pass(PassArgs a) {
         cx<T> twp[TWN];
         pass_stages<T, R, C, MODE, NTS, LP, 0, VPT>(a, lds, v, pre, tid, tile, twp);
     }
+#ifdef PIFFT_WG_CLOCK
+    if (a.wg_clock) {
+        __builtin_amdgcn_s_waitcnt(0);  // this thread's stores are done
+        __syncthreads();
+        if (tid == 0) {
+            a.wg_clock[3 * blockIdx.x + 1] = wall_clock64();
+            a.wg_clock[3 * blockIdx.x + 2] = __smid();
+        }
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
