@@ -543,11 +543,17 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         const int fvpt = env_int("PIFFT_FUSED_VPT", (pc.R <= 512 && wgs <= 128) ? 8 : 16);
         if (fvpt != pc.vpt && find_pass(prec, pc.R, pc.C, 3, pc.nts, heavy_lp, fvpt)) pc.vpt = fvpt;
     }
-    // tuning: lines per workgroup of the last pass (its write side's segment width)
-    const int last_c = env_int("PIFFT_LAST_C", 0);
-    if (last_c > 0 && out.size() > 1 &&
-        find_pass(prec, out.back().R, last_c, out.back().mode, out.back().nts, 0, out.back().vpt))
-        out.back().C = last_c;
+    // tuning: lines per workgroup (its write side's segment width) and values
+    // per thread of the last pass
+    const int last_c = env_int("PIFFT_LAST_C", 0), last_vpt = env_int("PIFFT_LAST_VPT", 0);
+    if ((last_c > 0 || last_vpt > 0) && out.size() > 1) {
+        PassChoice& b = out.back();
+        const int c = last_c > 0 ? last_c : b.C, v = last_vpt > 0 ? last_vpt : b.vpt;
+        if (find_pass(prec, b.R, c, b.mode, b.nts, 0, v)) {
+            b.C = c;
+            b.vpt = v;
+        }
+    }
     return 0;
 }
 
