@@ -90,11 +90,16 @@ for R in (256, 512):
     for nts in (0, 1):
         items.append(f"PKV(double, 64, {R}, 8, 10, {nts}, 0, 8),")
 # (trial, round 4: the last pass of config 2's one-GPU slice -- 128
-# one-wave workgroups at VPT 16 -- at 8 values per thread, PIFFT_LAST_VPT)
+# one-wave workgroups at VPT 16 -- at 8 or 4 values per thread,
+# PIFFT_LAST_VPT; and the slice's fused tree pass at 4, PIFFT_FUSED_VPT)
 for R in (256, 512):
     for C in (4, 8):
         for nts in (0, 1):
             items.append(f"PKV(double, 64, {R}, {C}, 2, {nts}, 0, 8),")
+    for nts in (0, 1):
+        items.append(f"PKV(double, 64, {R}, 4, 2, {nts}, 0, 4),")
+        for lp in (2, 3, 4):  # (at P = 2 a round of 16 leaf loads exceeds 4 values)
+            items.append(f"PKV(double, 64, {R}, 4, 3, {nts}, {lp}, 4),")
 # (blocked intermediates between the 2^28 passes -- the reading pass's tile a
 # contiguous region -- were built and lost 4-14 %: the writer's scattered
 # stores cost more than the reader gained; round 4,
