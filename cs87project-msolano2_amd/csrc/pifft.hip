@@ -543,6 +543,17 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
         const int fvpt = env_int("PIFFT_FUSED_VPT", (pc.R <= 512 && wgs <= 128) ? 8 : 16);
         if (fvpt != pc.vpt && find_pass(prec, pc.R, pc.C, 3, pc.nts, heavy_lp, fvpt)) pc.vpt = fvpt;
     }
+    // The last strided pass of a small fp64 plan (R <= 512, <= 256
+    // workgroups) at 8 values per thread too: measured on MI355X
+    // (profiles/r04k_slice.log, r04k_shapes.log) config 2's one-GPU slice
+    // 12.7 -> 12.2 us (+3.8 %), fp64 slices of local 2^16-2^19 +1.6-5 %, P = 1
+    // 2^16-2^18 +5-6 %; 4 values per thread +2.6 % (slice).  PIFFT_LAST_VPT:
+    // the values per thread instead (tuning, below).
+    if (prec == 64 && out.size() > 1 && out.back().mode == 2 && out.back().vpt == 16) {
+        PassChoice& pc = out.back();
+        const uint64_t wgs = (ntrans * (M / (uint64_t)pc.R) + pc.C - 1) / (uint64_t)pc.C;
+        if (pc.R <= 512 && wgs <= 256 && find_pass(prec, pc.R, pc.C, 2, pc.nts, 0, 8)) pc.vpt = 8;
+    }
     // tuning: lines per workgroup (its write side's segment width) and values
     // per thread of the last pass
     const int last_c = env_int("PIFFT_LAST_C", 0), last_vpt = env_int("PIFFT_LAST_VPT", 0);
@@ -637,6 +648,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         // the planned C or the widest instantiated one below it
         PassChoice& l = passes.back();
         const int bm = l.mode, cmin = bm == 0 ? 1 : 4;
+        if (l.vpt == 8 && !find_pass(p->prec, l.R, l.C, bm | 4, l.nts, 0, 8)) l.vpt = 16;  // (no VPT-8 twin)
         int C = l.C;
         while (C > cmin && !find_pass(p->prec, l.R, C, bm | 4, l.nts, 0, l.vpt)) C /= 2;
         if (!find_pass(p->prec, l.R, C, bm | 4, l.nts, 0, l.vpt))

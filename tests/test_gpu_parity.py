@@ -559,13 +559,13 @@ def test_fused_tree_first_pass(suf, logn, P, monkeypatch):
         assert rel_l2(run(plain, x), got) <= tol(suf, n)
 
 
-@pytest.mark.parametrize("env", [{"PIFFT_FUSED_VPT": "4"}, {"PIFFT_LAST_VPT": "8"}, {"PIFFT_LAST_VPT": "4"},
-                                 {"PIFFT_FUSED_VPT": "4", "PIFFT_LAST_VPT": "8"}, {"PIFFT_LAST_VPT": "8", "PIFFT_LAST_C": "8"}])
+@pytest.mark.parametrize("env,last_vpt", [({}, 8), ({"PIFFT_LAST_VPT": "16"}, 16),
+                                          ({"PIFFT_LAST_VPT": "8", "PIFFT_LAST_C": "8"}, 8)])
 @pytest.mark.parametrize("logn,P", [(20, 8), (18, 4), (21, 16)])
-def test_slice_pass_forms_vs_oracle(logn, P, env, monkeypatch):
-    """One-worker fp64 slices with the fused tree pass at 4 values per thread
-    and the last pass at 8 or 4 (tuning forms, round 4): every form matches
-    the oracle, and is the form the variables asked for."""
+def test_slice_last_pass_forms_vs_oracle(logn, P, env, last_vpt, monkeypatch):
+    """One-worker fp64 slices (config 2's shape and neighbours): the last
+    strided pass runs at 8 values per thread by default (round 4), at 16 or
+    at C = 8 under the tuning variables -- every form matches the oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 1 << logn
@@ -574,10 +574,7 @@ def test_slice_pass_forms_vs_oracle(logn, P, env, monkeypatch):
     for q in sorted({0, P - 1}):
         plan = pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0)
         d = plan.describe()
-        if "PIFFT_FUSED_VPT" in env:
-            assert d["launch_kind"][0] == "tree+pass" and d["vpt"][0] == int(env["PIFFT_FUSED_VPT"]), d
-        if "PIFFT_LAST_VPT" in env:
-            assert d["vpt"][-1] == int(env["PIFFT_LAST_VPT"]), d
+        assert d["launch_kind"] == ["tree+pass", "pass"] and d["vpt"][-1] == last_vpt, d
         assert_bins_close(run(plan, x), pifft_dist.slice_of_natural(want, P, q), "f64", n)
 
 

@@ -256,13 +256,18 @@ def test_small_slices_run_the_fused_pass_at_8_values_per_thread():
     """Round 4 (profiles/r04d_fused_vpt8.log): a one-worker slice's fused tree
     pass runs at 8 values per thread when it has R <= 512 points and at most
     128 workgroups (config 2's slice: 14.05 -> 12.66 us); R = 1024 and larger
-    launches keep 16; config-2-sized worker-interleaved passes run at 8."""
+    launches keep 16; config-2-sized worker-interleaved passes run at 8.  And
+    (profiles/r04k_*.log) the last strided pass of a small fp64 plan -- R <=
+    512, <= 256 workgroups -- runs at 8 too (the slice 12.7 -> 12.2 us)."""
     d = pifft.dry_run(1 << 20, 8, 1, F64, first=0, count=1)   # config 2's slice: 512 x 256, 64 workgroups
-    assert d["launch_kind"][0] == "tree+pass" and d["radix"] == [512, 256] and d["vpt"] == [8, 16]
+    assert d["launch_kind"][0] == "tree+pass" and d["radix"] == [512, 256] and d["vpt"] == [8, 8]
     assert d["launch_mode"] == [3, 2]
-    assert pifft.dry_run(1 << 21, 8, 1, F64, first=7, count=1)["vpt"] == [8, 16]   # 128 workgroups
-    assert pifft.dry_run(1 << 20, 2, 1, F64, first=0, count=1)["vpt"] == [16, 16]  # R = 1024 first
-    assert pifft.dry_run(1 << 23, 8, 1, F64, first=0, count=1)["vpt"] == [16, 16]  # 256 workgroups
+    assert pifft.dry_run(1 << 21, 8, 1, F64, first=7, count=1)["vpt"] == [8, 8]   # 128 workgroups each
+    assert pifft.dry_run(1 << 20, 2, 1, F64, first=0, count=1)["vpt"] == [16, 8]  # R = 1024 first
+    assert pifft.dry_run(1 << 23, 8, 1, F64, first=0, count=1)["vpt"] == [16, 16]  # 256 workgroups, R = 1024
     assert pifft.dry_run(1 << 28, 8, 1, F64, first=0, count=1)["vpt"] == [16, 16, 16]
+    assert pifft.dry_run(1 << 17, 1, 1, F64)["vpt"] == [16, 8]                    # P = 1: the last pass only
+    assert pifft.dry_run(1 << 20, 1, 1, F64)["vpt"] == [16, 16]                   # config 1 (R = 1024)
+    assert pifft.dry_run(1 << 17, 1, 1, F32)["vpt"] == [16, 16]                   # fp64 only
     assert pifft.dry_run(1 << 20, 8, 1, F64)["vpt"] == [8, 8]                     # config 2 (worker-interleaved)
     assert pifft.dry_run(1 << 28, 8, 1, F64)["vpt"] == [16, 16, 16]

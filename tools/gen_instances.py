@@ -89,17 +89,17 @@ for T, prec in (("double", 64), ("float", 32)):
 for R in (256, 512):
     for nts in (0, 1):
         items.append(f"PKV(double, 64, {R}, 8, 10, {nts}, 0, 8),")
-# (trial, round 4: the last pass of config 2's one-GPU slice -- 128
-# one-wave workgroups at VPT 16 -- at 8 or 4 values per thread,
-# PIFFT_LAST_VPT; and the slice's fused tree pass at 4, PIFFT_FUSED_VPT)
+# The last strided pass of small fp64 plans (R <= 512, <= 256 workgroups) at
+# 8 values per thread (round 4, profiles/r04k_slice.log, r04k_shapes.log:
+# config 2's slice +3.8 %, slices of local 2^16-2^19 +1.6-5 %, P = 1
+# 2^16-2^18 +5-6 %), and at C = 8 for PIFFT_LAST_C (tuning).
+# (4 values per thread: the slice's last pass +2.6 %, below 8; its fused
+# tree pass -4 %, local 2^17-2^18 fused passes -6-9 %, +5-7 % only at local
+# 2^15-2^16: not instantiated)
 for R in (256, 512):
     for C in (4, 8):
         for nts in (0, 1):
             items.append(f"PKV(double, 64, {R}, {C}, 2, {nts}, 0, 8),")
-    for nts in (0, 1):
-        items.append(f"PKV(double, 64, {R}, 4, 2, {nts}, 0, 4),")
-        for lp in (2, 3, 4):  # (at P = 2 a round of 16 leaf loads exceeds 4 values)
-            items.append(f"PKV(double, 64, {R}, 4, 3, {nts}, {lp}, 4),")
 # (blocked intermediates between the 2^28 passes -- the reading pass's tile a
 # contiguous region -- were built and lost 4-14 %: the writer's scattered
 # stores cost more than the reader gained; round 4,
