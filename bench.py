@@ -548,7 +548,9 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             job = Job(pifft, torch, gpu, n=n, P=g["P"], prec=g["prec"], first=g["first"], count=g["count"],
                       batch_local=g["batch"], b_first=0, seed=seed)
             # small steps: more of them, so the timed loop is not launch-jitter
-            k = max(steps, 50) if g["log_n"] < 24 else max(steps, 20)
+            # and its start (the first launch after a synchronize, ~10-20 us)
+            # is amortized: 200 steps of the 10-50 us configs take 2-10 ms
+            k = max(steps, 200) if g["log_n"] < 24 else max(steps, 20)
             elapsed = job.run(k, max(warmup, 5))
             ms = elapsed * 1e3 / k
             # the 10-50 us configs: 200 samples per launch (a few ms), so their
@@ -661,7 +663,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
         rec = {"workload": what}
         try:
             job = Job(pifft, torch, gpu, n=1 << log_n, prec=prec, seed=seed, **g)
-            k = max(steps, 50)
+            k = max(steps, 200)  # (as the one-GPU secondaries: the loop start amortized)
             local_s = job.run(k, max(warmup, 5), barrier)
             elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
             ms = elapsed * 1e3 / k
