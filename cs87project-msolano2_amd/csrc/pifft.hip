@@ -539,12 +539,6 @@ int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& 
     // values per thread instead (tuning).
     if (heavy_lp && !out.empty() && out[0].mode == 1) {
         PassChoice& pc = out[0];
-        // tuning: the fused pass's lines per workgroup (PIFFT_FUSED_C)
-        const int fc = env_int("PIFFT_FUSED_C", 0);
-        if (fc > 0 && find_pass(prec, pc.R, fc, 3, pc.nts, heavy_lp, 8)) {
-            pc.C = fc;
-            pc.vpt = 8;
-        }
         const uint64_t wgs = (ntrans * (M / (uint64_t)pc.R) + pc.C - 1) / (uint64_t)pc.C;
         const int fvpt = env_int("PIFFT_FUSED_VPT", (pc.R <= 512 && wgs <= 128) ? 8 : 16);
         if (fvpt != pc.vpt && find_pass(prec, pc.R, pc.C, 3, pc.nts, heavy_lp, fvpt)) pc.vpt = fvpt;

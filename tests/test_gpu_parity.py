@@ -560,13 +560,12 @@ def test_fused_tree_first_pass(suf, logn, P, monkeypatch):
 
 
 @pytest.mark.parametrize("env,last_vpt", [({}, 8), ({"PIFFT_LAST_VPT": "16"}, 16),
-                                          ({"PIFFT_LAST_VPT": "8", "PIFFT_LAST_C": "8"}, 8), ({"PIFFT_FUSED_C": "2"}, 8)])
+                                          ({"PIFFT_LAST_VPT": "8", "PIFFT_LAST_C": "8"}, 8)])
 @pytest.mark.parametrize("logn,P", [(20, 8), (18, 4), (21, 16)])
 def test_slice_last_pass_forms_vs_oracle(logn, P, env, last_vpt, monkeypatch):
     """One-worker fp64 slices (config 2's shape and neighbours): the last
     strided pass runs at 8 values per thread by default (round 4), at 16 or
-    at C = 8 under the tuning variables, and the fused tree pass at C = 2
-    (trial) -- every form matches the oracle."""
+    at C = 8 under the tuning variables -- every form matches the oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 1 << logn
@@ -576,8 +575,6 @@ def test_slice_last_pass_forms_vs_oracle(logn, P, env, last_vpt, monkeypatch):
         plan = pifft.Plan(n, P, 1, pifft.F64, first=q, count=1, device=0)
         d = plan.describe()
         assert d["launch_kind"] == ["tree+pass", "pass"] and d["vpt"][-1] == last_vpt, d
-        if "PIFFT_FUSED_C" in env:
-            assert d["lines"][0] == int(env["PIFFT_FUSED_C"]) and d["vpt"][0] == 8, d
         assert_bins_close(run(plan, x), pifft_dist.slice_of_natural(want, P, q), "f64", n)
 
 

@@ -100,13 +100,10 @@ for R in (256, 512):
     for C in (4, 8):
         for nts in (0, 1):
             items.append(f"PKV(double, 64, {R}, {C}, 2, {nts}, 0, 8),")
-# (trial, round 4: config 2's slice with its fused tree pass at C = 2 --
-# 128 workgroups, twice the CUs gathering leaves, 32-B leaf segments;
-# PIFFT_FUSED_C=2)
-for R in (256, 512):
-    for nts in (0, 1):
-        for lp in (2, 3, 4):
-            items.append(f"PKV(double, 64, {R}, 2, 3, {nts}, {lp}, 8),")
+# (config 2's slice with its fused tree pass at C = 2 -- 128 workgroups
+# gathering leaves, 32-B leaf segments: +0.7 % on the slice, 0 to +2.4 % on
+# neighbouring slices, within run-to-run noise; round 4,
+# profiles/r04n_fused_c2.log; not instantiated)
 # (blocked intermediates between the 2^28 passes -- the reading pass's tile a
 # contiguous region -- were built and lost 4-14 %: the writer's scattered
 # stores cost more than the reader gained; round 4,
