@@ -551,7 +551,7 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             # and its start (the first launch after a synchronize, ~10-20 us)
             # is amortized: 200 steps of the 10-50 us configs take 2-10 ms
             k = max(steps, 200) if g["log_n"] < 24 else max(steps, 20)
-            elapsed = job.run(k, max(warmup, 5))
+            elapsed = job.run(k, max(warmup, k // 4))  # (a warm-up of a quarter of the loop: the clocks settle)
             ms = elapsed * 1e3 / k
             # the 10-50 us configs: 200 samples per launch (a few ms), so their
             # means hold to ~1 % against the rocprofv3 trace
@@ -664,7 +664,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
         try:
             job = Job(pifft, torch, gpu, n=1 << log_n, prec=prec, seed=seed, **g)
             k = max(steps, 200)  # (as the one-GPU secondaries: the loop start amortized)
-            local_s = job.run(k, max(warmup, 5), barrier)
+            local_s = job.run(k, max(warmup, k // 4), barrier)
             elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
             ms = elapsed * 1e3 / k
             job.time_launches(200)
