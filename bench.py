@@ -550,8 +550,8 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             # small steps: more of them, so the timed loop is not launch-jitter
             # and its start (the first launch after a synchronize, ~10-20 us)
             # is amortized: 200 steps of the 10-50 us configs take 2-10 ms
-            k = max(steps, 200) if g["log_n"] < 24 else max(steps, 20)
-            elapsed = job.run(k, max(warmup, k // 4))  # (a warm-up of a quarter of the loop: the clocks settle)
+            k = max(steps, int(os.environ.get("BENCH_SMALL_STEPS", "200"))) if g["log_n"] < 24 else max(steps, 20)
+            elapsed = job.run(k, max(warmup, int(os.environ.get("BENCH_SMALL_WARMUP", str(k // 4)))))  # (a quarter of the loop)
             ms = elapsed * 1e3 / k
             # the 10-50 us configs: 200 samples per launch (a few ms), so their
             # means hold to ~1 % against the rocprofv3 trace
