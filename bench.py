@@ -547,10 +547,12 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
             n = 1 << g["log_n"]
             job = Job(pifft, torch, gpu, n=n, P=g["P"], prec=g["prec"], first=g["first"], count=g["count"],
                       batch_local=g["batch"], b_first=0, seed=seed)
-            # small steps: more of them, so the timed loop is not launch-jitter
-            # and its start (the first launch after a synchronize, ~10-20 us)
-            # is amortized: 200 steps of the 10-50 us configs take 2-10 ms
-            k = max(steps, int(os.environ.get("BENCH_SMALL_STEPS", "200"))) if g["log_n"] < 24 else max(steps, 20)
+            # small steps: more of them, so the timed loop is the steady state:
+            # 1000 steps of the 10-50 us configs (10-45 ms, after 250 warm-up
+            # steps).  Measured on one box (profiles/r04r_loop_length.txt):
+            # 50 / 200 / 1000 steps -> config 3 45.4 / 48.2 / 44.4 us, config
+            # 2's slice 12.6 / 12.3 / 12.25 us, config 2 30.0 / 29.4 / 29.1 us
+            k = max(steps, int(os.environ.get("BENCH_SMALL_STEPS", "1000"))) if g["log_n"] < 24 else max(steps, 20)
             elapsed = job.run(k, max(warmup, int(os.environ.get("BENCH_SMALL_WARMUP", str(k // 4)))))  # (a quarter of the loop)
             ms = elapsed * 1e3 / k
             # the 10-50 us configs: 200 samples per launch (a few ms), so their
@@ -663,7 +665,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
         rec = {"workload": what}
         try:
             job = Job(pifft, torch, gpu, n=1 << log_n, prec=prec, seed=seed, **g)
-            k = max(steps, 200)  # (as the one-GPU secondaries: the loop start amortized)
+            k = max(steps, 1000)  # (as the one-GPU secondaries: the steady state)
             local_s = job.run(k, max(warmup, k // 4), barrier)
             elapsed = pifft_dist.max_over_ranks(local_s, red_dev)
             ms = elapsed * 1e3 / k
