@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--prec", type=int, default=64, choices=(32, 64))
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--reps", type=int, default=20, help="clocked launches per pass (medians reported)")
+    ap.add_argument("--dump", default="", help="CSV of every workgroup of every clocked launch (launch, rep, wg, "
+                                               "start_us, end_us, hw_id; times from the launch's first entry)")
     args = ap.parse_args()
     L = pifft.lib()
     f = L.pifft_debug_wg_clock
@@ -57,6 +59,9 @@ def main():
     ev = [plan.execute_device_timed(x.data_ptr(), y.data_ptr(), st) for _ in range(args.reps)]
     print(f"n=2^{args.log_n} P={args.workers} count={count} fp{args.prec} batch={args.batch}: "
           f"launches {d['launch_kind']}, radix {d['radix']}")
+    dump = open(args.dump, "w") if args.dump else None
+    if dump:
+        dump.write("launch,rep,wg,start_us,end_us,hw_id\n")
     for li in range(d["num_launches"]):
         name = plan.kernel_name(li)
         buf = (ctypes.c_ulonglong * (3 * 65536))()
@@ -72,6 +77,10 @@ def main():
             t0 = [buf[3 * w] for w in range(nwg)]
             t1 = [buf[3 * w + 1] for w in range(nwg)]
             durs = sorted((b - a) * us for a, b in zip(t0, t1))
+            if dump:
+                m0 = min(t0)
+                for w in range(nwg):
+                    dump.write(f"{li},{len(rows)},{w},{(t0[w] - m0) * us:.2f},{(t1[w] - m0) * us:.2f},{buf[3 * w + 2]}\n")
             rows.append(((max(t0) - min(t0)) * us, durs[0], statistics.median(durs), durs[-1],
                          (max(t1) - min(t0)) * us, len({buf[3 * w + 2] for w in range(nwg)})))
         if not rows:
