@@ -804,7 +804,8 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #define PIFFT_TREE_LOADS_SMALL 16  // the same for tiles of <= 256 threads
 #endif
                 constexpr int TL = PassCfg<R, C, VPT>::NT <= 256 ? PIFFT_TREE_LOADS_SMALL : PIFFT_TREE_LOADS;
-                constexpr int G = P >= TL ? 1 : TL / P;
+                constexpr int G0 = P >= TL ? 1 : TL / P;
+                constexpr int G = G0 > q ? q : G0;  // (at most one round per value)
                 static_assert(q % G == 0, "whole rounds of leaf loads");
                 const uint32_t log_m = log_lb + Sh::LOGR;
                 const uint32_t wq = a.worker + (uint32_t)(tile * C >> log_lb & ((1u << a.log_nq) - 1));
