@@ -229,7 +229,7 @@ def test_position_model_not_for_worker_interleaved_plans():
 STRAY = {"PIFFT_ORDER": "1", "PIFFT_PASSES": "4", "PIFFT_RADIX_LOGS": "10,10,8", "PIFFT_NT": "0",
          "PIFFT_WORKER_IL": "0", "PIFFT_POS_MODEL": "0", "PIFFT_VPT32": "0", "PIFFT_W_PAD": "0",
          "PIFFT_TILE64": "4096", "PIFFT_LAST_C": "16", "PIFFT_FUSE_TREE": "0", "PIFFT_ILV": "1",
-         "PIFFT_SINGLE_TILE32": "8192"}
+         "PIFFT_SINGLE_TILE32": "8192", "PIFFT_LAST_VPT": "16", "PIFFT_FUSED_VPT": "16", "PIFFT_WIL_VPT": "16"}
 
 
 @pytest.mark.parametrize("shape", [(1 << 28, 1, 1, F64, 0, 1, 0), (1 << 28, 1, 1, F32, 0, 1, 0),
