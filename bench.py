@@ -985,6 +985,7 @@ def main() -> int:
                 "batch_per_gpu": b_count, "shard": args.shard,
                 "local_n": desc["local_n"], "passes": desc["num_passes"], "radix": desc["radix"],
                 "lines_per_workgroup": desc["lines"],
+                "kernel_names": [job.plan.kernel_name(i) for i in range(desc["num_launches"])],
                 "hbm_bytes_per_step_algorithmic": total_bytes,
                 "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                 "launches": launches,

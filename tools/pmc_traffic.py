@@ -14,10 +14,13 @@ Recipe (MI355X_MICROARCH.md, HBM / rocprofv3 PMC slots):
     once, yet raw FETCH_SIZE is 0.500x those bytes in all three passes -- the
     same half count -> x2 as well (WRITE_SIZE: 1.000x, exact).
 
-Runs bench.py under each counter pass, maps the timed loop's dispatches to
-the plan's launch indices (the plan's launches repeat in order every step),
-and writes profiles/<tag>_traffic.json, which bench.py reads for
-roofline.traffic.
+Runs bench.py under each counter pass, finds every full execution of the
+plan among the dispatches (its launches in order, by the kernel names the
+bench line records -- bench.py's single-kernel roofline loops are left out),
+averages each launch over them, and writes profiles/<tag>_traffic.json,
+which bench.py reads for roofline.traffic.  (Round 4, r04w: the earlier
+"last steps x launches dispatches" rule took the roofline loops' dispatches
+once bench.py added them.)
 
 usage: python tools/pmc_traffic.py --tag r01 [bench.py args...]
 """
@@ -114,15 +117,33 @@ def main() -> None:
         launches = line["config"]["launches"]
         nl = len(launches)
         disp = [d for d in per_dispatch(rows, counter) if any(o in d[1] for o in OURS)]
-        timed = disp[-args.steps * nl:]
+        names = line["config"].get("kernel_names")
+        if names:
+            # every full execution of the plan: nl consecutive dispatches with
+            # the plan's kernels in order (workspace tuning, warm-up, timed and
+            # profiling loops; not bench.py's single-kernel roofline loops)
+            execs, i = [], 0
+            while i + nl <= len(disp):
+                if all(disp[i + j][1] == names[j] for j in range(nl)):
+                    execs.append(disp[i:i + nl])
+                    i += nl
+                else:
+                    i += 1
+            if not execs:
+                raise SystemExit(f"no full execution of {names} among {len(disp)} dispatches")
+        else:  # (lines before round 4: the timed loop is the tail)
+            tail = disp[-args.steps * nl:]
+            execs = [tail[s * nl:(s + 1) * nl] for s in range(len(tail) // nl)]
         for i in range(nl):
-            vals = [timed[s * nl + i][2] for s in range(args.steps) if s * nl + i < len(timed)]
-            per_launch[i][counter] = sum(vals) / max(len(vals), 1)
-            per_launch[i]["kernel"] = timed[i][1] if i < len(timed) else "?"
+            vals = [e[i][2] for e in execs]
+            per_launch[i][counter] = sum(vals) / len(vals)
+            per_launch[i]["kernel"] = execs[-1][i][1]
+        per_launch[0].setdefault("executions", {})[counter] = len(execs)
         result["counters"][counter] = len(disp)
     cfg = line["config"]
     key = f"n2^{cfg['n'].bit_length() - 1}_f{b.prec}_b{cfg['batch']}_P{cfg['workers']}_q{cfg['workers_per_gpu']}"
     result["config_key"] = key
+    result["executions_averaged"] = per_launch[0].get("executions")
     result["bench_line"] = line
     nl = len(cfg["launches"])
     launch_bytes = [l.get("bytes") for l in cfg["launches"]]
