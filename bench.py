@@ -904,6 +904,7 @@ def main() -> int:
     job.time_launches(max(5, args.steps // 2))  # after the timed region
     rf = job.roofline(local_s * 1e3 / args.steps)
     desc = job.desc
+    kernel_names = [job.plan.kernel_name(i) for i in range(desc["num_launches"])]
     launches = job.launches(local_s * 1e3 / args.steps)
     config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
     traffic, traffic_src = load_traffic(config_key, rf["launches"],
@@ -985,7 +986,7 @@ def main() -> int:
                 "batch_per_gpu": b_count, "shard": args.shard,
                 "local_n": desc["local_n"], "passes": desc["num_passes"], "radix": desc["radix"],
                 "lines_per_workgroup": desc["lines"],
-                "kernel_names": [job.plan.kernel_name(i) for i in range(desc["num_launches"])],
+                "kernel_names": kernel_names,
                 "hbm_bytes_per_step_algorithmic": total_bytes,
                 "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                 "launches": launches,
