@@ -10,6 +10,7 @@ scratch order (tmp_in, CPU.c:463-478).  Tolerances as in test_gpu_parity.py
 (north star: rel-L2 1e-12 fp64, 1e-5 log2 N fp32, every bin against the
 typical bin magnitude).  Sizes stay within a few seconds of oracle time.
 """
+import os
 import random
 
 import numpy as np
@@ -24,7 +25,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-def _cases(count=48, seed=20261017):
+def _cases(count=int(os.environ.get("FUZZ_COUNT", "48")), seed=int(os.environ.get("FUZZ_SEED", "20261017"))):
+    # (FUZZ_COUNT / FUZZ_SEED: a longer sweep on demand, e.g. profiles/r04zb_fuzz_seed4242.txt)
     rng = random.Random(seed)
     out = []
     while len(out) < count:
