@@ -93,7 +93,7 @@ def test_random_plan_padded_workspace_bitwise(suf, logn, P, first, count, batch,
     assert outs[0] == outs[1]
 
 
-def _large_cases(count=8, seed=4242):
+def _large_cases(count=int(os.environ.get("FUZZ_LARGE_COUNT", "8")), seed=int(os.environ.get("FUZZ_LARGE_SEED", "4242"))):
     rng = random.Random(seed)
     out = []
     for _ in range(count):
@@ -115,7 +115,7 @@ def test_random_large_plan_vs_oracle(suf, logn, P, first, count, batch, flags):
     test_random_plan_vs_oracle(suf, logn, P, first, count, batch, flags)
 
 
-def _wil_cases(count=16, seed=20261018):
+def _wil_cases(count=int(os.environ.get("FUZZ_WIL_COUNT", "16")), seed=int(os.environ.get("FUZZ_WIL_SEED", "20261018"))):
     """Natural-order all-worker shapes with P <= 16 and a multi-pass local FFT
     (M = N/P >= 2^15): the worker-interleaved layout's domain."""
     rng = random.Random(seed)
