@@ -483,8 +483,19 @@ class Job:
         step_bytes = sum(d["launch_bytes"][:nl])
         rec["step_achieved"] = round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1) if ms_per_step > 0 else None
         rec["step_frac"] = round(rec["step_achieved"] / HBM_PEAK_GBS, 4) if rec["step_achieved"] else None
-        # self-check: the kernel's launches, back to back, cannot take longer
-        # than the step they run in (beyond REFUSE_TOL)
+        # self-checks, both recorded: the dominant kernel's launches, back to
+        # back, cannot take longer than the step they run in (beyond
+        # REFUSE_TOL: refused), and every kernel function's clean loop
+        # together -- and the sampled per-launch event times -- should fit in
+        # it too (recorded, with the tolerance, so a reader sees when the
+        # tolerance was used)
+        loops_ms = sum(shares.values()) if shares else dom_step_ms
+        rec["loops_ms_per_step"] = round(loops_ms, 6)
+        rec["checks"] = {"tol": REFUSE_TOL,
+                         "dominant_fits_step": bool(dom_step_ms <= ms_per_step),
+                         "dominant_fits_step_tol": bool(dom_step_ms <= ms_per_step * (1 + REFUSE_TOL)),
+                         "all_loops_fit_step_tol": bool(loops_ms <= ms_per_step * (1 + REFUSE_TOL)),
+                         "sampled_events_fit_step": bool(raw_step_ms <= ms_per_step)}
         if dom_ms <= 0 or dom_step_ms > ms_per_step * (1 + REFUSE_TOL):
             rec.update({"achieved": None, "frac": None,
                         "error": f"refused: the kernel's {len(dom_launches)} launches take {dom_step_ms:.6f} ms "
@@ -633,14 +644,12 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
     rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
                 "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(local_s * 1e3 / steps),
                 "roofline_rank0": job.roofline(local_s * 1e3 / steps) if rank == 0 else None})
-    prep = verify_prepare(pifft, torch, dist, job, rank, world)
-    job.x = None  # the 64 GiB replica is not needed by the exchange
-    job.plan.close()  # nor the plan's workspace
-    torch.cuda.empty_cache()
-    ag_ms, natural = allgather(pifft, torch, dist, job, barrier, red_dev, keep=rank == 0)
-    rec["allgather_ms"] = round(ag_ms, 3)
-    rec["verify"] = verify_finish(torch, prep, natural)
-    del natural, prep
+
+    def _drop_replica():
+        job.x = None  # the 64 GiB replica is not needed by the exchange
+        job.plan.close()  # nor the plan's workspace
+        torch.cuda.empty_cache()
+    exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, rec, between=_drop_replica)
     job.free()
     return rec
 
@@ -675,10 +684,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
                         "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"],
                         "roofline_rank0": job.roofline(local_s * 1e3 / k) if rank == 0 else None})
             if g["count"] < g["P"]:  # a worker split: check it (slices bitwise, gathered result vs one GPU)
-                prep = verify_prepare(pifft, torch, dist, job, rank, world)
-                _, natural = allgather(pifft, torch, dist, job, barrier, red_dev, keep=rank == 0)
-                rec["verify"] = verify_finish(torch, prep, natural)
-                del natural, prep
+                exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, rec)
             job.free()
         except Exception as e:  # reported, never silently replaced
             rec["error"] = repr(e)
@@ -710,6 +716,7 @@ def verify_prepare(pifft, torch, dist, job, rank: int, world: int) -> dict:
     dist.all_gather_object(digests, pifft_dist.tensor_digest(job.y))
     if rank != 0:
         return {}
+    _fault("verify", rank)
     st = job.stream
     same = []
     for q in range(world):
@@ -775,6 +782,41 @@ def verify_finish(torch, prep: dict, natural) -> dict | None:
     return rec
 
 
+def exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, rec: dict, verify: bool = True,
+                        gather: bool = True, between=None) -> None:
+    """The optional stages after a multi-GPU timed loop, none of which may
+    cost the line (round-4 verdict): the split's self-check (verify_prepare,
+    rank 0 replaying the other ranks' plans), the all-gather + interleave
+    and the comparison of the gathered result.  Every failure becomes
+    rec["verify_error"] / rec["allgather_error"]; after each stage the ranks
+    agree (all_ranks_ok, one all-reduce) whether to go on, so a stage that
+    failed on one rank only (rank 0's replay running out of HBM, say) never
+    leaves the others waiting in a collective.  `between`: run after the
+    preparation (config 5 frees its replica there)."""
+    prep = None
+    if verify:
+        prep = guarded(rec, "verify_error", verify_prepare, pifft, torch, dist, job, rank, world)
+        if not all_ranks_ok("verify_error" not in rec, dist, red_dev):
+            rec.setdefault("verify_error", "skipped: the self-check failed on another rank")
+            prep = None
+    if between is not None:
+        between()
+    natural = None
+    if gather:
+        def _exchange():
+            ms, nat = allgather(pifft, torch, dist, job, barrier, red_dev, keep=prep is not None and rank == 0)
+            _fault("allgather", rank)
+            return ms, nat
+        got = guarded(rec, "allgather_error", _exchange)
+        if all_ranks_ok(got is not None, dist, red_dev):
+            rec["allgather_ms"] = round(got[0], 3)
+            natural = got[1]
+        else:
+            rec.setdefault("allgather_error", "skipped: the exchange failed on another rank")
+    if prep is not None and "allgather_error" not in rec:
+        rec["verify"] = guarded(rec, "verify_error", verify_finish, torch, prep, natural if gather else None)
+
+
 def allgather(pifft, torch, dist, job, barrier, red_dev, keep: bool = False):
     """The optional final exchange: RCCL all-gather of every rank's result,
     then -- for a worker split -- the stride-P interleave into natural order on
@@ -800,6 +842,131 @@ def allgather(pifft, torch, dist, job, barrier, red_dev, keep: bool = False):
     ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
     del gathered
     return ms, (natural if keep else None)
+
+
+# ---------------------------------------------------------------------------
+# The printed line and its sidecar.  The driver keeps the last ~8 KB of
+# stdout (round-4 verdict: the ~15 KB line lost configs 1 and 2 from the
+# record), so the line carries each config's numbers only -- value, step,
+# roofline {kernel_name, mean_ms, frac, traffic}, cpu_baseline {value, cores,
+# ms} -- and the per-launch detail goes to a sidecar JSON (--detail).
+LINE_MAX_CHARS = 7000
+
+_RF_KEYS = ("bound", "kernel_name", "launches", "mean_ms", "loop_reps", "trace_loop_dispatches", "achieved",
+            "peak", "unit", "frac", "traffic", "algorithmic_bytes", "kernel_ms_per_step", "all_launches_ms_per_step",
+            "step_ms", "step_frac", "checks", "error")
+_RF_SECONDARY = ("kernel_name", "launches", "mean_ms", "loop_reps", "trace_loop_dispatches", "achieved", "peak",
+                 "frac", "traffic", "algorithmic_bytes", "step_frac", "error")
+_CPU_KEYS = ("value", "unit", "cores", "kind", "ms", "sample", "cpu_model", "cpu_share", "error")
+
+
+def _pick(d, keys):
+    return None if d is None else {k: d[k] for k in keys if k in d}
+
+
+def _short_sample(cb: dict) -> dict:
+    """cpu_baseline for the line: the sample's first clause (what ran, at what
+    size and p) stands for the full prose kept in the sidecar."""
+    out = _pick(cb, _CPU_KEYS)
+    if out and isinstance(out.get("sample"), str):
+        out["sample"] = out["sample"].split(";")[0][:160]
+    alt = cb.get("alternative") if cb else None
+    if alt:
+        out["alternative"] = _pick(alt, ("value", "cores", "ms", "error"))
+    return out
+
+
+def compact_secondary(sec: dict | None) -> dict | None:
+    if not sec:
+        return sec
+    out = {}
+    for key, rec in sec.items():
+        c = {k: rec[k] for k in ("value", "ms_per_step", "dtype", "n", "workers", "workers_in_plan", "batch",
+                                 "batch_per_gpu", "n_gpus", "allgather_ms", "hbm_need_GiB", "hbm_free_GiB",
+                                 "error", "allgather_error") if k in rec}
+        for rk in ("roofline", "roofline_rank0"):
+            if rec.get(rk) is not None:
+                c[rk] = _pick(rec[rk], _RF_SECONDARY)
+                if isinstance(rec[rk].get("checks"), dict):  # (each check in the sidecar)
+                    c[rk]["checks_ok"] = all(v for k, v in rec[rk]["checks"].items() if k != "tol" and
+                                             k != "sampled_events_fit_step")
+        if "cpu_baseline" in rec:
+            cb = rec["cpu_baseline"] or {}
+            c["cpu_baseline"] = _pick(cb, ("value", "cores", "kind", "ms", "error"))
+        if rec.get("verify") is not None:
+            c["verify"] = _pick(rec["verify"], ("ok", "slices_bitwise", "slices_checked", "rel_l2", "bins_ok",
+                                                "bins_max_err", "error", "note"))
+        out[key] = c
+    return out
+
+
+def compact_line(full: dict) -> dict:
+    """The printed line: the contract's keys, the headline config's numbers
+    and each secondary config's summary; lists of launches and prose go to
+    the sidecar (config.detail names it)."""
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    cfg = full["config"]
+    c = {k: cfg[k] for k in ("workload", "n", "workers", "workers_per_gpu", "batch", "batch_per_gpu", "shard",
+                             "local_n", "passes", "parallelism", "hbm_GBps_per_step_algorithmic", "allgather_ms",
+                             "allgather_error", "verify_error", "per_rank_error", "emulated_rank", "stage",
+                             "detail") if k in cfg}
+    if cfg.get("verify") is not None:
+        c["verify"] = _pick(cfg["verify"], ("ok", "slices_bitwise", "slices_checked", "rel_l2", "bins_ok",
+                                            "bins_max_err", "error", "note"))
+    if cfg.get("per_rank") is not None:
+        c["per_rank"] = [_pick(r, ("rank", "ms_per_step", "dominant_ms", "frac")) for r in cfg["per_rank"]]
+    if cfg.get("secondary") is not None:
+        c["secondary"] = compact_secondary(cfg["secondary"])
+    line["config"] = c
+    line["roofline"] = _pick(full["roofline"], _RF_KEYS)
+    line["cpu_baseline"] = _short_sample(full["cpu_baseline"]) if full.get("cpu_baseline") else full.get("cpu_baseline")
+    return line
+
+
+def emit(full: dict, detail_path: str | None) -> str:
+    """Writes the full record to the sidecar, prints the compact line (one
+    line, flushed) and returns it.  A line still over LINE_MAX_CHARS drops
+    its secondary summaries' verify objects, then the per-rank list."""
+    if detail_path:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail_path)), exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(full, f, indent=1)
+        except OSError as e:
+            full["config"]["detail"] = f"not written: {e!r}"
+    line = compact_line(full)
+    s = json.dumps(line)
+    if len(s) > LINE_MAX_CHARS:
+        for rec in (line["config"].get("secondary") or {}).values():
+            rec.pop("verify", None)
+        s = json.dumps(line)
+    if len(s) > LINE_MAX_CHARS and line["config"].get("per_rank"):
+        line["config"]["per_rank"] = "in the sidecar"
+        s = json.dumps(line)
+    print(s, flush=True)
+    return s
+
+
+def guarded(rec: dict, key: str, fn, *a, **kw):
+    """fn(*a, **kw), an exception becoming rec[key] (repr) and None: the
+    optional stages after the timed region never cost the line."""
+    try:
+        return fn(*a, **kw)
+    except Exception as e:  # reported, never silently replaced
+        rec[key] = repr(e)[:400]
+        return None
+
+
+def _fault(stage: str, rank: int) -> None:
+    """Test-only fault injection (BENCH_FAULT=<stage>[:rank]): raises in that
+    stage on that rank (default rank 0), to check that the line survives."""
+    spec = os.environ.get("BENCH_FAULT", "")
+    if not spec:
+        return
+    st, _, r = spec.partition(":")
+    if st == stage and rank == int(r or 0):
+        raise RuntimeError(f"injected fault in {stage} on rank {rank} (BENCH_FAULT)")
 
 
 def main() -> int:
@@ -834,6 +1001,10 @@ def main() -> int:
     ap.add_argument("--as-rank", default="",
                     help="q/G: run only rank q's plan of a G-GPU job, on this one GPU and without a process "
                          "group (per-rank profiling, e.g. tools/pmc_traffic.py); never a job-level number")
+    ap.add_argument("--detail", default=os.environ.get("BENCH_DETAIL", os.path.join(ROOT, "gpurun_out",
+                                                                                   "bench_detail.json")),
+                    help="sidecar JSON with the full record (per-launch times, kernel names, prose); the printed "
+                         "line keeps each config's numbers ('' = none)")
     args = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
@@ -907,111 +1078,110 @@ def main() -> int:
     kernel_names = [job.plan.kernel_name(i) for i in range(desc["num_launches"])]
     launches = job.launches(local_s * 1e3 / args.steps)
     config_key = f"n2^{args.log_n}_f{args.prec}_b{b_count}_P{P}_q{count}"
-    traffic, traffic_src = load_traffic(config_key, rf["launches"],
-                                        [job.plan.kernel_name(i) for i in rf["launches"]])
-
-    per_rank = None
-    if dist is not None:
-        mine = {"rank": rank, "gpu": gpu, "workers": [first, first + count], "batch": [b_first, b_first + b_count],
-                "ms_per_step": round(local_s * 1e3 / args.steps, 6), "dominant_ms": rf["mean_ms"],
-                "achieved": rf["achieved"], "frac": rf["frac"]}
-        per_rank = [None] * world
-        dist.all_gather_object(per_rank, mine)
-
-    allgather_ms = verify = None
-    prep = None
-    if dist is not None and args.shard == "workers" and count < P:
-        prep = verify_prepare(pifft, torch, dist, job, rank, world)
-    if args.allgather and dist is not None and (args.shard == "batch" or count < P):
-        allgather_ms, natural = allgather(pifft, torch, dist, job, barrier, red_dev, keep=prep is not None and rank == 0)
-        if prep is not None:
-            verify = verify_finish(torch, prep, natural)
-        del natural
-    elif prep is not None:
-        verify = verify_finish(torch, prep, None)
-    prep = None
-    job.free()
-
-    secondary = None
-    if not args.no_secondary and not emulated:
-        if world == 1 and args.log_n == 28 and args.prec == 64 and args.batch == 1:
-            secondary = secondary_configs(pifft, torch, gpu, args.steps, args.warmup, args.seed, args.cpu_threads,
-                                          not args.no_cpu_baseline)
-        elif world > 1 and args.shard == "workers":
-            secondary = multi_secondary(pifft, torch, dist, gpu, rank, world, args.steps, args.warmup, args.seed,
-                                        barrier, red_dev)
-            if world == 8:  # (config5 refuses cleanly when the HBM cannot hold it, e.g. a 1-GPU rehearsal at 2^32)
-                try:
-                    secondary["C5"] = config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
-                                              min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n,
-                                              same_device=args.same_device)
-                except Exception as e:  # reported, never silently replaced
-                    secondary["C5"] = {"error": repr(e)}
+    rf["traffic"], rf["traffic_source"] = load_traffic(config_key, rf["launches"],
+                                                       [job.plan.kernel_name(i) for i in rf["launches"]])
 
     total_bytes = sum(desc["launch_bytes"][: desc["num_launches"]])
     flops = 5.0 * n * args.log_n * args.batch  # the whole job's batch (every rank's share)
     value = flops / (ms_per_step * 1e-3) / 1e9
+    full = {
+        "metric": _baseline_metric(),
+        "value": round(value, 2),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 6),
+        "higher_is_better": True,
+        "scaling": "strong",  # the job's total work (one transform, or the global batch) is fixed
+        "vs_baseline": None,
+        "dtype": "f64" if prec == pifft.F64 else "f32",
+        "data": "synthetic: splitmix64 U[-1,1]/sqrt(N) complex input generated in HBM (the oracle's generator)",
+        "config": {
+            "workload": (f"config 4: one fp64 complex N=2^{args.log_n} pi-FFT" if args.log_n == 28 and
+                         args.prec == 64 and args.batch == 1 else
+                         f"config 3: batched fp32 {args.batch} x N=4096" if args.log_n == 12 and
+                         args.prec == 32 and args.batch == 4096 else
+                         f"pi-FFT N=2^{args.log_n} f{args.prec} batch {args.batch}")
+                        + (f", P={P} workers, {b_count} whole transforms per GPU (batch-sharded, no "
+                           f"data-path collective)" if args.shard == "batch" else
+                           f", P={P} workers, {count} per GPU (no data-path collective)"),
+            "n": n, "workers": P, "workers_per_gpu": count, "batch": args.batch,
+            "batch_per_gpu": b_count, "shard": args.shard,
+            "local_n": desc["local_n"], "passes": desc["num_passes"], "radix": desc["radix"],
+            "lines_per_workgroup": desc["lines"],
+            "kernel_names": kernel_names,
+            "hbm_bytes_per_step_algorithmic": total_bytes,
+            "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            "launches": launches,
+            "parallelism": (f"batch-split {args.batch}/{world} per GPU, p{P}" if args.shard == "batch" else
+                            f"pi-split p{P} over {world} GPU(s)"),
+            "allgather_ms": None,
+            "verify": None,
+            "per_rank": None,
+            "emulated_rank": args.as_rank or None,
+            "secondary": None,
+            "detail": os.path.relpath(args.detail, ROOT) if args.detail else None,
+        },
+        "roofline": rf,
+        "cpu_baseline": None,
+    }
+    cfg = full["config"]
+    if dist is not None and rank == 0:
+        # the headline is complete here: print it before anything optional
+        # runs (the first multi-GPU run executes the RCCL exchange for the
+        # first time; CPU.c:485-492, worker 0 reports regardless of the
+        # others).  The final line below repeats it with the rest.
+        cfg["stage"] = "headline (the final line follows)"
+        emit(full, args.detail)
+    cfg["stage"] = None
+
+    if dist is not None:
+        mine = {"rank": rank, "gpu": gpu, "workers": [first, first + count], "batch": [b_first, b_first + b_count],
+                "ms_per_step": round(local_s * 1e3 / args.steps, 6), "dominant_ms": rf["mean_ms"],
+                "achieved": rf["achieved"], "frac": rf["frac"]}
+
+        def _gather_rows():
+            rows = [None] * world
+            dist.all_gather_object(rows, mine)
+            return rows
+        cfg["per_rank"] = guarded(cfg, "per_rank_error", _gather_rows)
+
+    # the optional exchange and the split's self-check (exchange_and_verify:
+    # every failure an *_error field, all ranks on the same branch)
+    if dist is not None and (args.shard == "batch" or count < P):
+        exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, cfg,
+                            verify=args.shard == "workers" and count < P, gather=args.allgather)
+    job.free()
+
+    if not args.no_secondary and not emulated:
+        if world == 1 and args.log_n == 28 and args.prec == 64 and args.batch == 1:
+            cfg["secondary"] = secondary_configs(pifft, torch, gpu, args.steps, args.warmup, args.seed,
+                                                 args.cpu_threads, not args.no_cpu_baseline)
+        elif world > 1 and args.shard == "workers":
+            sec = guarded(cfg, "secondary_error", multi_secondary, pifft, torch, dist, gpu, rank, world,
+                          args.steps, args.warmup, args.seed, barrier, red_dev)
+            if sec is not None and world == 8:  # (config5 refuses cleanly when the HBM cannot hold it)
+                try:
+                    sec["C5"] = config5(pifft, torch, dist, gpu, rank, world, min(args.steps, 5),
+                                        min(args.warmup, 2), args.seed, barrier, red_dev, args.c5_log_n,
+                                        same_device=args.same_device)
+                except Exception as e:  # reported, never silently replaced
+                    sec["C5"] = {"error": repr(e)[:400]}
+            cfg["secondary"] = sec
+
     if rank == 0:
-        rf_line = {k: rf[k] for k in ("bound", "kernel", "kernel_name", "launches", "mean_ms", "loop_reps",
-                                      "trace_loop_dispatches", "sampled_mean_ms", "achieved", "peak", "unit", "frac")}
-        rf_line.update({"traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": rf["algorithmic_bytes"],
-                        "kernel_ms_per_step": rf["kernel_ms_per_step"],
-                        "all_launches_ms_per_step": rf["all_launches_ms_per_step"], "step_ms": rf["step_ms"],
-                        "step_achieved": rf["step_achieved"], "step_frac": rf["step_frac"]})
-        if "error" in rf:
-            rf_line["error"] = rf["error"]
-        line = {
-            "metric": _baseline_metric(),
-            "value": round(value, 2),
-            "unit": "GFLOP/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 6),
-            "higher_is_better": True,
-            "scaling": "strong",  # the job's total work (one transform, or the global batch) is fixed
-            "vs_baseline": None,
-            "dtype": "f64" if prec == pifft.F64 else "f32",
-            "data": "synthetic: splitmix64 U[-1,1]/sqrt(N) complex input generated in HBM (the oracle's generator)",
-            "config": {
-                "workload": (f"config 4: one fp64 complex N=2^{args.log_n} pi-FFT" if args.log_n == 28 and
-                             args.prec == 64 and args.batch == 1 else
-                             f"config 3: batched fp32 {args.batch} x N=4096" if args.log_n == 12 and
-                             args.prec == 32 and args.batch == 4096 else
-                             f"pi-FFT N=2^{args.log_n} f{args.prec} batch {args.batch}")
-                            + (f", P={P} workers, {b_count} whole transforms per GPU (batch-sharded, no "
-                               f"data-path collective)" if args.shard == "batch" else
-                               f", P={P} workers, {count} per GPU (no data-path collective)"),
-                "n": n, "workers": P, "workers_per_gpu": count, "batch": args.batch,
-                "batch_per_gpu": b_count, "shard": args.shard,
-                "local_n": desc["local_n"], "passes": desc["num_passes"], "radix": desc["radix"],
-                "lines_per_workgroup": desc["lines"],
-                "kernel_names": kernel_names,
-                "hbm_bytes_per_step_algorithmic": total_bytes,
-                "hbm_GBps_per_step_algorithmic": round(total_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                "launches": launches,
-                "parallelism": (f"batch-split {args.batch}/{world} per GPU, p{P}" if args.shard == "batch" else
-                                f"pi-split p{P} over {world} GPU(s)"),
-                "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),
-                "verify": verify,
-                "per_rank": per_rank,
-                "emulated_rank": args.as_rank or None,
-                "secondary": secondary,
-            },
-            "roofline": rf_line,
-            "cpu_baseline": None,
-        }
         # rank 0 of every job (also N > 1, so the driver's scaling lines carry
         # it), after the GPU work: the other ranks do not wait for it
         if not emulated and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = headline_cpu_baseline(args.cpu_log_n or args.log_n, args.prec,
+                full["cpu_baseline"] = headline_cpu_baseline(args.cpu_log_n or args.log_n, args.prec,
                                                              batch=args.batch, threads=args.cpu_threads or None)
             except Exception as e:  # reported, never silently replaced
-                line["cpu_baseline"] = {"value": None, "error": repr(e)}
-        print(json.dumps(line), flush=True)
+                full["cpu_baseline"] = {"value": None, "error": repr(e)}
+        emit(full, args.detail)
     if dist is not None:
-        dist.destroy_process_group()
+        guarded({}, "destroy", dist.destroy_process_group)
     return 0
 
 

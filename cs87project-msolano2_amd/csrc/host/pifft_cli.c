@@ -401,12 +401,14 @@ out:
 }
 
 /* CPU.c:312-380: the P workers go to t->gpus GPUs, P/gpus consecutive workers
- * each, and run concurrently; no data moves between GPUs. */
+ * each, and run concurrently; no data moves between GPUs.  Returns 0, -1 on
+ * an error (as the reference's run), or 1 when -t -g G's split check ran and
+ * failed (main exits with EXIT_FAILURE on anything but 0). */
 int run(tr_t* t) {
     pifft_plan* plans[1024] = {0};
     const uint32_t G = t->gpus;
     const uint32_t per = t->P / G;
-    int rc = -1;
+    int rc = -1, split = 0;
     double s1 = 0, s2 = 0;
     if (initialize_data(t)) goto done;
     const int sep = t->separate_tree ? PIFFT_SEPARATE_TREE : 0;
@@ -455,7 +457,15 @@ int run(tr_t* t) {
     } else {
         print_output(t);
         verify_results(t);
-        if (G > 1 && check_split(t, plans) < 0) goto done;
+        if (G > 1) {
+            /* test-only (PIFFT_TUNING=1 PIFFT_FAULT=split_check): one wrong
+             * output bit, so the failing branch of the check runs */
+            const char* tu = getenv("PIFFT_TUNING");
+            const char* fa = getenv("PIFFT_FAULT");
+            if (tu && !strcmp(tu, "1") && fa && !strcmp(fa, "split_check")) ((unsigned char*)t->out)[0] ^= 1;
+            split = check_split(t, plans);
+            if (split < 0) goto done;
+        }
     }
     if (t->dump) {
         FILE* f = fopen(t->dump, "wb");
@@ -466,12 +476,13 @@ int run(tr_t* t) {
         }
         fclose(f);
     }
-    rc = 0;
+    /* a failed split check ran to the end but is not a success: exit status 1 */
+    rc = split ? 1 : 0;
 done:
     for (uint32_t g = 0; g < G; g++)
         if (plans[g]) pifft_plan_destroy(plans[g]);
     cleanup_data(t);
-    if (rc) stderr_out("Could not run the transform\n");
+    if (rc < 0) stderr_out("Could not run the transform\n");
     return rc;
 }
 

@@ -72,6 +72,16 @@ int env_int(const char* name, int dflt) {
     return (s && *s) ? atoi(s) : dflt;
 }
 
+// Test-only fault injection for the multi-GPU error paths, which a one-GPU
+// box cannot otherwise reach (tests/test_gpu_parity.py): PIFFT_FAULT=<site>
+// (enable_peer, peer_copy, broadcast), read only under PIFFT_TUNING=1, makes
+// that call fail as a HIP error would.
+bool fault_at(const char* site) {
+    if (!tuning_on()) return false;
+    const char* s = getenv("PIFFT_FAULT");
+    return s && !strcmp(s, site);
+}
+
 // Timing events only time (pifft_execute_device_timed, pifft_profile_*,
 // pifft_execute_group's stage timers): no system-scope fence when they are
 // recorded, so a timed kernel does not pay an L2 write-back at its end (a
@@ -187,6 +197,7 @@ struct pifft_plan {
     void* d_hin = nullptr;   // pifft_execute's staging copies
     void* d_hout = nullptr;
     void* d_gather = nullptr;  // pifft_allgather: every worker's slices on this plan's device
+    void* d_nat = nullptr;  // pifft_execute_group: the gathered natural-order result (d_hin keeps the input)
     std::vector<char> host_tmp;
     std::vector<int> peer_on;  // devices this plan's device has peer access to (pifft_allgather)
     std::vector<hipStream_t> gst;  // pifft_allgather: one copy stream per source plan
@@ -577,6 +588,7 @@ void release(pifft_plan* p) {
     if (p->d_hin) (void)hipFree(p->d_hin);
     if (p->d_hout) (void)hipFree(p->d_hout);
     if (p->d_gather) (void)hipFree(p->d_gather);
+    if (p->d_nat) (void)hipFree(p->d_nat);
     for (auto st : p->gst) (void)hipStreamDestroy(st);
     for (auto e : p->gdone) (void)hipEventDestroy(e);
     for (auto e : p->gev)
@@ -1194,6 +1206,8 @@ int check_cover(pifft_plan* const* plans, int np, bool quiet) {
 // peer access from plan d's device to `src_dev` (xGMI loads/copies without a
 // host bounce); a pair that cannot peer still copies, staged by the runtime
 int enable_peer(pifft_plan* d, int src_dev) {
+    if (fault_at("enable_peer"))
+        return fail("hipDeviceEnablePeerAccess(%d -> %d): injected fault (PIFFT_FAULT=enable_peer)", d->device, src_dev);
     if (src_dev == d->device) return 0;
     for (int e : d->peer_on)
         if (e == src_dev) return 0;
@@ -1248,8 +1262,8 @@ int gather_group(pifft_plan* const* plans, int np, const void* const* d_slices, 
         has_dst.push_back(d_natural[i] != nullptr);
     }
     const GatherSchedule gs = gather_schedule(srcs, has_dst, N, M, p0->batch);
-    for (int j = 0; j < np; j++) {
-        if (!d_natural[j]) continue;
+    // one destination's copies + interleave, enqueued (no host wait)
+    auto enqueue = [&](int j) -> int {
         pifft_plan* d = plans[j];
         DeviceGuard g(d->device);
         if (!d->d_gather) HIPCHK(hipMalloc(&d->d_gather, (size_t)d->batch * N * esz));
@@ -1270,6 +1284,9 @@ int gather_group(pifft_plan* const* plans, int np, const void* const* d_slices, 
         for (const GatherCopy& c : gs.copies) {
             if (c.dst != j) continue;
             const pifft_plan* s = plans[c.src];
+            if (fault_at("peer_copy"))
+                return fail("hipMemcpyPeerAsync(%d <- %d): injected fault (PIFFT_FAULT=peer_copy)", d->device,
+                            s->device);
             HIPCHK(hipMemcpyPeerAsync((char*)d->d_gather + c.dst_off * esz, d->device,
                                       (const char*)d_slices[c.src] + c.src_off * esz, s->device, c.elems * esz,
                                       d->gst[c.stream]));
@@ -1280,6 +1297,24 @@ int gather_group(pifft_plan* const* plans, int np, const void* const* d_slices, 
         }
         if (launch_interleave(d->d_gather, d_natural[j], N, d->P, d->batch, d->prec, d->stream)) return -1;
         HIPCHK(hipEventRecord(d->gev[1], d->stream));
+        return 0;
+    };
+    for (int j = 0; j < np; j++) {
+        if (!d_natural[j] || !enqueue(j)) continue;
+        // a failure part-way: wait for what was already enqueued (copies
+        // still reading the caller's slices, or writing a gather buffer)
+        // before returning, so the caller may reuse its buffers and the plans
+        // stay usable; the first error's message is kept
+        const std::string msg = g_err;
+        for (int k = 0; k <= j; k++) {
+            if (!d_natural[k]) continue;
+            DeviceGuard g(plans[k]->device);
+            for (auto st : plans[k]->gst) (void)hipStreamSynchronize(st);
+            (void)hipStreamSynchronize(plans[k]->stream);
+        }
+        (void)hipGetLastError();
+        g_err = msg;
+        return -1;
     }
     double worst = 0.0;
     for (int j = 0; j < np; j++) {
@@ -1639,12 +1674,29 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
         HIPCHK(hipMemcpyAsync(p0->d_hin, host_in, in_bytes, hipMemcpyHostToDevice, p0->stream));
         HIPCHK(hipStreamSynchronize(p0->stream));
     }
-    for (int i = 1; i < np; i++) {
+    // (a failure part-way waits for the broadcast copies already enqueued --
+    // they read plans[0]'s staging buffer, which the next call overwrites)
+    auto broadcast = [&](int i) -> int {
         pifft_plan* p = plans[i];
         DeviceGuard g(p->device);
         if (ensure_host_staging(p)) return -1;
         if (enable_peer(p, plans[0]->device)) return -1;
+        if (fault_at("broadcast"))
+            return fail("hipMemcpyPeerAsync(%d <- %d): injected fault (PIFFT_FAULT=broadcast)", p->device,
+                        plans[0]->device);
         HIPCHK(hipMemcpyPeerAsync(p->d_hin, p->device, plans[0]->d_hin, plans[0]->device, in_bytes, p->stream));
+        return 0;
+    };
+    for (int i = 1; i < np; i++) {
+        if (!broadcast(i)) continue;
+        const std::string msg = g_err;
+        for (int k = 1; k < i; k++) {
+            DeviceGuard g(plans[k]->device);
+            (void)hipStreamSynchronize(plans[k]->stream);
+        }
+        (void)hipGetLastError();
+        g_err = msg;
+        return -1;
     }
     for (int i = 1; i < np; i++) {
         DeviceGuard g(plans[i]->device);
@@ -1675,16 +1727,22 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
     if (host_out) {
         if (np > 1 && check_cover(plans, np, true) == 0) {
             // the whole transform over several plans: gather on the first
-            // plan's device (pifft_allgather; its input staging copy is free
-            // now and takes the natural-order result) and copy back once
+            // plan's device (pifft_allgather) into a plan-owned result
+            // buffer -- not the input staging copy, which
+            // pifft_execute_group_kernel_times re-runs the plans on -- and
+            // copy back once
+            pifft_plan* p = plans[0];
+            {
+                DeviceGuard g(p->device);
+                if (!p->d_nat) HIPCHK(hipMalloc(&p->d_nat, (size_t)p->batch * p->n * p->esz));
+            }
             std::vector<const void*> sl(np);
             std::vector<void*> nat(np, nullptr);
             for (int i = 0; i < np; i++) sl[i] = plans[i]->d_hout;
-            nat[0] = plans[0]->d_hin;
+            nat[0] = p->d_nat;
             if (gather_group(plans, np, sl.data(), nat.data(), nullptr)) return -1;
-            pifft_plan* p = plans[0];
             DeviceGuard g(p->device);
-            HIPCHK(hipMemcpy(host_out, p->d_hin, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(host_out, p->d_nat, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToHost));
             return 0;
         }
         for (int i = 0; i < np; i++) {

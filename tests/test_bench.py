@@ -13,13 +13,40 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(*args):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
-                       timeout=240, cwd=ROOT)
+LINE_MAX_CHARS = 7000  # bench.LINE_MAX_CHARS: the driver keeps the last ~8 KB of stdout
+
+
+def _bench(*args, env_extra=None, tmp=None):
+    """Runs bench.py; checks the printed line (one at N = 1; at N > 1 the
+    headline first, printed before the optional exchange, then the final
+    line) and returns the full record from its sidecar (--detail), with the
+    printed line under "_line"."""
+    import tempfile
+    side = os.path.join(tmp or tempfile.mkdtemp(), "detail.json")
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args, "--detail", side],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    return json.loads(lines[0])
+    multi = "--gpus" in args and args[args.index("--gpus") + 1] != "1"
+    assert len(lines) == (2 if multi else 1), r.stdout
+    for ln in lines:
+        assert len(ln) <= LINE_MAX_CHARS, len(ln)
+    line = json.loads(lines[-1])
+    if multi:
+        first = json.loads(lines[0])
+        assert first["config"]["stage"].startswith("headline") and line["config"].get("stage") is None
+        assert first["value"] == line["value"] and first["ms_per_step"] == line["ms_per_step"]
+    with open(side) as f:
+        d = json.load(f)
+    assert d["value"] == line["value"] and d["ms_per_step"] == line["ms_per_step"]
+    assert line["roofline"].get("frac") == d["roofline"].get("frac")
+    for key, rec in (d["config"].get("secondary") or {}).items():  # every config's numbers are in the line
+        lrec = line["config"]["secondary"][key]
+        assert lrec.get("value") == rec.get("value") and lrec.get("ms_per_step") == rec.get("ms_per_step")
+    d["_line"] = line
+    return d
 
 
 def _common(d, steps, warmup, n_gpus=1):
@@ -37,6 +64,7 @@ def _common(d, steps, warmup, n_gpus=1):
     assert abs(d["value"] - flops / (d["ms_per_step"] * 1e-3) / 1e9) <= tol
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert set(rf["checks"]) >= {"tol", "dominant_fits_step_tol", "all_loops_fit_step_tol"}
     _roofline_ok(rf, d["ms_per_step"] if n_gpus == 1 else None, contended=n_gpus > 1)
     assert len(d["config"]["launches"]) >= 1
 
@@ -159,3 +187,15 @@ def test_bench_secondary_configs():
     assert sec["C4_f32"]["dtype"] == "f32" and sec["C4_f32"]["n"] == 1 << 28
     assert sec["C3"]["dtype"] == "f32" and sec["C3"]["batch"] == 4096
     assert sec["C2"]["workers"] == 8 and sec["C2_slice"]["workers_in_plan"] == 1
+
+
+def test_bench_exchange_failure_keeps_the_line():
+    """An injected failure in the exchange (BENCH_FAULT, rank 0 after the
+    collective) on a 2-rank rehearsal: both lines print, the final one with
+    allgather_error, value and ms_per_step, and no rank hangs."""
+    d = _bench("--gpus", "2", "--same-device", "--dist-backend", "gloo", "--log-n", "18", "--steps", "2",
+               "--warmup", "1", "--no-cpu-baseline", "--no-secondary", env_extra={"BENCH_FAULT": "allgather:0"})
+    line = d["_line"]
+    assert line["value"] > 0 and line["ms_per_step"] > 0
+    assert "injected" in line["config"]["allgather_error"] and line["config"]["allgather_ms"] is None
+    assert line["config"].get("verify") is None

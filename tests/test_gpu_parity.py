@@ -463,9 +463,11 @@ def test_large_fp64_linearity():
 
 
 # -------------------------------------------------------------------- CLI ---
-def _cli(args):
+def _cli(args, env=None):
     import subprocess
-    return subprocess.run([pifft.CLI_PATH] + args, capture_output=True, text=True, timeout=300)
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([pifft.CLI_PATH] + args, capture_output=True, text=True, timeout=300, env=e)
 
 
 @pytest.mark.parametrize("prec", ["32", "64"])
@@ -529,6 +531,11 @@ def test_cli_split_checks_itself(args):
     assert r.returncode == 0, r.stderr
     assert "Split check passed." in r.stdout, r.stdout[-400:]
     assert "replayed bit for bit: yes" in r.stdout
+    # a failing check is a failing run (round-4 advice): one output bit flipped
+    # (test-only PIFFT_FAULT=split_check) -> "FAILED" and a non-zero exit status
+    r = _cli(["-t", "-n", "4096"] + args + ["-R"], env={"PIFFT_TUNING": "1", "PIFFT_FAULT": "split_check"})
+    assert "Split check FAILED." in r.stdout, r.stdout[-400:]
+    assert r.returncode == 1 and "Could not run" not in r.stderr, (r.returncode, r.stderr)
 
 
 @pytest.mark.parametrize("P", ["1", "2", "8"])
@@ -900,6 +907,51 @@ def test_allgather_errors():
     other = pifft.Plan(n * 2, P, 1, pifft.F64, first=3, count=1, device=0)
     with pytest.raises(pifft.PifftError, match="share"):
         pifft.allgather(plans[:3] + [other], [b.data_ptr() for b in bufs], [nat.data_ptr(), None, None, None])
+
+
+@pytest.mark.parametrize("site", ["enable_peer", "broadcast", "peer_copy"])
+def test_multi_gpu_error_paths_fail_cleanly(site, monkeypatch):
+    """The multi-GPU error branches (peer access, the xGMI input broadcast of
+    pifft_execute_group, the peer copies of pifft_allgather), reached on one
+    GPU through the test-only fault switch (PIFFT_TUNING=1 PIFFT_FAULT=<site>):
+    each call returns -1 with the message (CPU.c:102-109's -1 + message), holds
+    no more device memory afterwards than before, and the next call on the
+    same plans succeeds with the same bytes."""
+    n, P, batch = 1 << 16, 8, 2
+    x = oracle.generate(n * batch, np.complex128, seed=31)
+    plans = [pifft.Plan(n, P, batch, pifft.F64, first=q, count=1, device=0) for q in range(P)]
+    want = np.zeros(n * batch, np.complex128)
+    pifft.execute_group(plans, x, want)  # allocates the staging and gather buffers and the copy streams
+    st = torch.cuda.current_stream()
+    d_in = dev(x)
+    slices = [torch.empty(p.info.out_elems, dtype=d_in.dtype, device="cuda") for p in plans]
+    for p, sl in zip(plans, slices):
+        p.execute_device(d_in.data_ptr(), sl.data_ptr(), st)
+    nat = torch.empty(n * batch, dtype=d_in.dtype, device="cuda")
+    pifft.allgather(plans, [sl.data_ptr() for sl in slices], [nat.data_ptr()] + [None] * (P - 1))
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    monkeypatch.setenv("PIFFT_TUNING", "1")
+    monkeypatch.setenv("PIFFT_FAULT", site)
+    got = np.zeros(n * batch, np.complex128)
+    with pytest.raises(pifft.PifftError, match="injected fault"):
+        if site == "peer_copy":
+            pifft.allgather(plans, [sl.data_ptr() for sl in slices], [nat.data_ptr()] + [None] * (P - 1))
+        else:
+            pifft.execute_group(plans, x, got)
+    assert "injected fault" in pifft.last_error()
+    if site == "peer_copy":  # the device gather inside execute_group fails the same way
+        with pytest.raises(pifft.PifftError, match="injected fault"):
+            pifft.execute_group(plans, x, got)
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info(0)[0] == free0
+    monkeypatch.delenv("PIFFT_FAULT")
+    pifft.execute_group(plans, x, got)
+    assert got.tobytes() == want.tobytes()
+    nat2 = torch.empty_like(nat)
+    pifft.allgather(plans, [sl.data_ptr() for sl in slices], [nat2.data_ptr()] + [None] * (P - 1))
+    torch.cuda.synchronize()
+    assert torch.equal(nat2, nat) and nat.cpu().numpy().tobytes() == want.tobytes()
 
 
 @pytest.mark.parametrize("suf", list(DT))

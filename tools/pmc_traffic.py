@@ -42,15 +42,15 @@ OURS = ("k_pass", "k_tree", "k_interleave")
 def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[dict], dict]:
     """rocprofv3 --pmc <counter> -- python bench.py ...; returns (rows, bench JSON line).
     This process never touches the GPU (rocprofv3 and bench.py are children)."""
+    os.makedirs(outdir, exist_ok=True)
+    side = os.path.join(outdir, "bench_detail.json")
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
-           sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
+           sys.executable, os.path.join(ROOT, "bench.py")] + bench_args + ["--detail", side]
     r = subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.PIPE, text=True)
-    line = None
-    for ln in r.stdout.splitlines():
-        if ln.startswith("{") and '"metric"' in ln:
-            line = json.loads(ln)
-    if line is None:
+    if not any(ln.startswith("{") and '"metric"' in ln for ln in r.stdout.splitlines()):
         raise SystemExit("bench.py printed no JSON line")
+    with open(side) as f:  # the full record (per-launch bytes and kernel names): bench.py's sidecar
+        line = json.load(f)
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {outdir}")
