@@ -1339,6 +1339,8 @@ extern "C" {
 
 const char* pifft_last_error(void) { return g_err.c_str(); }
 
+int pifft_abi_version(void) { return PIFFT_ABI_VERSION; }
+
 int pifft_gpu_count(void) {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);

@@ -58,10 +58,13 @@ class PlanInfo(ctypes.Structure):
     ]
 
 
+ABI_VERSION = 3  # include/pifft.h PIFFT_ABI_VERSION: the pifft_plan_info layout PlanInfo mirrors
+
 # every symbol include/pifft.h declares, with its ctypes signature
 _P = ctypes.c_void_p
 _SIGS = {
     "pifft_last_error": (ctypes.c_char_p, []),
+    "pifft_abi_version": (ctypes.c_int, []),
     "pifft_gpu_count": (ctypes.c_int, []),
     "pifft_plan_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_int]),
@@ -125,6 +128,10 @@ def lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        # PlanInfo above mirrors this layout version of pifft_plan_info
+        if L.pifft_abi_version() != ABI_VERSION:
+            raise PifftError(f"{LIB_PATH}: ABI version {L.pifft_abi_version()}, this binding expects {ABI_VERSION} "
+                             f"(include/pifft.h PIFFT_ABI_VERSION; rebuild)")
         _lib = L
     return _lib
 

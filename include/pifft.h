@@ -71,6 +71,16 @@ typedef struct pifft_plan pifft_plan;
 
 #define PIFFT_MAX_LAUNCH_INFO 256 /* launches described by pifft_plan_info */
 
+/* Layout version of pifft_plan_info and of this header's entry points,
+ * bumped at every change a binding compiled against an older header would
+ * misread: 1 rounds 1-3; 2 round 4 (chunk_pairs removed, launch_mode added);
+ * 3 round 5 (pifft_abi_version added; the struct is unchanged from 2).  A
+ * binding checks pifft_abi_version() == the PIFFT_ABI_VERSION it was written
+ * against before reading a pifft_plan_info -- cs87project-msolano2_amd/pifft.py
+ * does. */
+#define PIFFT_ABI_VERSION 3
+int pifft_abi_version(void);
+
 typedef struct pifft_plan_info {
     uint64_t n;              /* transform length N                                */
     uint32_t workers;        /* P                                                 */
@@ -100,8 +110,8 @@ typedef struct pifft_plan_info {
                                 packed fp32 passes of large transforms)            */
     int32_t launch_mode[PIFFT_MAX_LAUNCH_INFO]; /* k_pass MODE of each pass launch (bits 0-1: single /
                                   first / later / fused-tree pass, 4 bit-reversed store, 8
-                                  worker-interleaved, 16 / 32 reads / writes the blocked
-                                  intermediate); 0 for tree and interleave launches */
+                                  worker-interleaved; other bits reserved, never set);
+                                  0 for tree and interleave launches */
     int32_t layout;          /* bit 0: worker-interleaved passes (all P <= 16 workers of a
                                 natural-order plan: the last pass writes natural order);
                                 bit 1: the last pass stores natural order from the

@@ -23,6 +23,16 @@ def test_exports_every_header_symbol():
         assert hasattr(L, name), name
 
 
+def test_abi_version_matches_the_header_and_binding():
+    """pifft_plan_info's layout version (round-4 advice: the struct changed
+    mid-way with no marker): the header's PIFFT_ABI_VERSION, the library's
+    pifft_abi_version() and the ctypes mirror's ABI_VERSION agree."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(pifft.LIB_PATH), "..", "include", "pifft.h")).read()
+    want = int(re.search(r"#define PIFFT_ABI_VERSION (\d+)", hdr).group(1))
+    assert pifft.lib().pifft_abi_version() == want == pifft.ABI_VERSION
+
+
 @pytest.mark.parametrize("n,P,msg", [
     (3, 1, "Invalid input size"),
     (1, 1, "Invalid input size"),
