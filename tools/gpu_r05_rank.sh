@@ -12,7 +12,7 @@ run() {  # g variants
   echo "== fp64 2^28, worker 0 of $1" >> "$out/rank_orders.log"
   timeout -k 10 240 python3 -u tools/tune.py --log-n 28 --prec 64 --workers $1 --first 0 --count 1 --steps 20 --warmup 5 --tune-ws 4 --variants "$2" 2>&1 | grep -v "amdgpu.ids" >> "$out/rank_orders.log"
 }
-run 8 '[{}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,8,9"}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,9,8"}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"7,9,9"}, {}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,8,9"}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"7,9,9"}]' || exit 1
-run 4 '[{}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,9,9"}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"7,9,10"}, {}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,9,9"}]' || exit 1
-run 2 '[{}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,9,10"}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,10,9"}, {}, {"PIFFT_TUNING":"1","PIFFT_RADIX_LOGS":"8,9,10"}]' || exit 1
+run 8 '[{}, {"PIFFT_RADIX_LOGS":"8,8,9"}, {"PIFFT_RADIX_LOGS":"8,9,8"}, {"PIFFT_RADIX_LOGS":"7,9,9"}, {"PIFFT_XCD_GROUP":"0"}, {"PIFFT_XCD_GROUP":"3"}, {"PIFFT_XCD_GROUP":"4"}, {}, {"PIFFT_RADIX_LOGS":"8,8,9"}, {"PIFFT_RADIX_LOGS":"7,9,9"}]' || exit 1
+run 4 '[{}, {"PIFFT_RADIX_LOGS":"8,9,9"}, {"PIFFT_RADIX_LOGS":"7,9,10"}, {}, {"PIFFT_RADIX_LOGS":"8,9,9"}]' || exit 1
+run 2 '[{}, {"PIFFT_RADIX_LOGS":"8,9,10"}, {"PIFFT_RADIX_LOGS":"8,10,9"}, {}, {"PIFFT_RADIX_LOGS":"8,9,10"}]' || exit 1
 cat "$out/rank_orders.log"
