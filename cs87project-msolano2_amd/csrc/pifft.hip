@@ -701,11 +701,29 @@ int build_plan(pifft_plan* p, bool dry = false) {
     size_t tree_direct = 0;
     TwoLevel tree2;
     bool tree_is_direct = false;
+    // The worker-interleaved plan's one tree launch (k_tree_wil) feeds its
+    // passes only -- its output is never observed, and the plan's result
+    // matches the oracle within tolerance either way -- so from 2^21 values
+    // up it takes the factored two-level twiddles (one small-table lookup per
+    // level and thread) instead of the reference-formula table, whose
+    // N (1 - 1/P) entries it otherwise reads beside the data (C2: 1.44x its
+    // algorithmic bytes, profiles/r05b_traffic_n2^20_f64_b1_P8_q8.json).
+    // Measured on MI355X (profiles/r05g_wil_tree.log): fp64 2^21 P = 8
+    // 46 -> 42 us, 2^22 P = 16 80 -> 70 us; but config 2 itself (fp64 2^20,
+    // P = 8: 512 workgroups, one round, latency-bound) 29 -> 31 us -- there
+    // the extra dependent fp64 products sit on the critical path -- and 2^18
+    // ties.  The stand-alone tree (pifft_tree_device) keeps the reference
+    // table and stays bitwise.  PIFFT_WIL_TREE_DIRECT=1: the reference table
+    // at every size (tuning, tests); PIFFT_WIL_TREE_MIN_LOG: the threshold.
+    bool wil_factored = false;
     if (need_tree) {
         const int direct_max = env_int("PIFFT_TREE_DIRECT_MAX_LOG", 22);
         if (p->log_n <= direct_max) {
             tree_is_direct = true;
             tree_direct = tb.reference_omega_levels(p->n, p->lp);
+            wil_factored = p->wil && env_int("PIFFT_WIL_TREE_DIRECT", 0) == 0 &&
+                           (uint64_t)p->batch * p->n >= (1ull << env_int("PIFFT_WIL_TREE_MIN_LOG", 21));
+            if (wil_factored) tree2 = two_level(tb, p->n);
         } else {
             tree2 = two_level(tb, p->n);
         }
@@ -801,6 +819,12 @@ int build_plan(pifft_plan* p, bool dry = false) {
                                           (const void*)&k_tree_wil<float, 3>, (const void*)&k_tree_wil<float, 4>};
             Step& t = e.steps.back();
             t.fn = p->prec == 64 ? tw64[p->lp] : tw32[p->lp];
+            if (wil_factored) {
+                t.ta.tw.direct = nullptr;
+                t.ta.tw.lo = twp(tree2.lo);
+                t.ta.tw.hi = twp(tree2.hi);
+                t.ta.tw.h = tree2.h;
+            }
             t.ta.out_bstride = p->n;
             t.lds = (size_t)tree_wil_pad(256u << p->lp) * esz;
             if (t.lds > 65536 && !dry) (void)hipFuncSetAttribute(t.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)t.lds);

@@ -779,6 +779,10 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
     for bt in range(batch):
         assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
     monkeypatch.setenv("PIFFT_WIL_VPT", "16")
+    # (the default plan's tree reads the factored two-level twiddles; with the
+    # reference-formula table -- the slice-major plan's -- the arithmetic is the
+    # slice-major plan's, bit for bit)
+    monkeypatch.setenv("PIFFT_WIL_TREE_DIRECT", "1")
     wil = pifft.Plan(n, P, batch, PREC[suf])
     assert wil.describe()["worker_interleaved"] and "interleave" not in wil.describe()["launch_kind"]
     assert set(wil.describe()["vpt"]) == {16}
