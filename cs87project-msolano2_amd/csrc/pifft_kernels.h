@@ -600,14 +600,20 @@ struct Stage {
     //     instead of an LDS store + load per component.
     //     PIFFT_PERMLANE bit 0: radix 2 (R = 512), bit 1: radix 4 (R = 1024).
     //     Measured on MI355X (tools/gpu_round.sh perm): radix 2 in the fused
-    //     tree pass ~0.5 % faster; radix 4 in the C4 first pass 5.5 % SLOWER
-    //     (1.815 vs 1.720 ms: the transposes push the kernel past 128 VGPRs,
-    //     2 spills), so only bit 0 is on by default.
+    //     tree pass ~0.5 % faster.  Radix 4 cost 2 spills and 5.5 % in round
+    //     1's C4 first pass; since round 3 it compiles spill-free wherever
+    //     the workgroup holds at most 4 lines or runs a plain first pass
+    //     (fp32 instances drop 4-16 VGPRs with it), while the fp64 single
+    //     passes at C = 8 / 16 and fused passes at C = 16 would spill 2-4
+    //     VGPRs (round 5, every instance's gfx950 register metadata with and
+    //     without it) -- so it is on there only (perm4_ok).  Config 1 +0.5-1 %
+    //     (profiles/r04c_permlane4_c1.log), bitwise equal to the LDS path.
 #ifndef PIFFT_PERMLANE
-#define PIFFT_PERMLANE 1
+#define PIFFT_PERMLANE 3
 #endif
+    static constexpr bool perm4_ok = C <= 4 || MODE == 1;
     static constexpr bool perm = last && !first && !cfast && Sh::Q == 16 && NT % 64 == 0 && Sh::NSTG == 3 &&
-                                 (((PIFFT_PERMLANE & 2) && q == 4 && NBP == 64) ||
+                                 (((PIFFT_PERMLANE & 2) && q == 4 && NBP == 64 && perm4_ok) ||
                                   ((PIFFT_PERMLANE & 1) && q == 2 && NBP == 32));
     __host__ __device__ static __forceinline__ void map(int tid, int u, int& c, int& b) {
         if constexpr (perm) {
