@@ -624,10 +624,9 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const bool wil_ok = p->natural && p->P > 1 && p->nq == p->P && p->lp <= 4 && env_int("PIFFT_WORKER_IL", 1);
     const bool may_fuse = p->P > 1 && p->nq == 1 && p->lp <= 4 && !p->separate_tree && env_int("PIFFT_FUSE_TREE", 1);
     if (plan_passes(p->m, p->prec, ntrans, passes, may_fuse ? p->lp : 0, true, !wil_ok)) return -1;
-    if (wil_ok && passes.size() > 1) {
-        // the same radices, every pass a worker-interleaved MODE 2 (| 8)
-        // pass at the C of a MODE 2 pass whose lines run over all workers
-        std::vector<PassChoice> w = passes;
+    // the same radices, every pass a worker-interleaved MODE 2 (| 8) pass at
+    // the C of a MODE 2 pass whose lines run over all workers
+    auto to_wil = [&](std::vector<PassChoice>& w) -> bool {
         bool ok = true;
         for (auto& pc : w) {
             const uint64_t lines = p->m / (uint64_t)pc.R;
@@ -650,9 +649,44 @@ int build_plan(pifft_plan* p, bool dry = false) {
             const int wvpt = env_int("PIFFT_WIL_VPT", small ? 8 : 16);
             if (wvpt != pc.vpt && find_pass(p->prec, pc.R, pc.C, pc.mode, pc.nts, 0, wvpt)) pc.vpt = wvpt;
         }
-        if (ok) {
+        return ok;
+    };
+    if (wil_ok && passes.size() > 1) {
+        std::vector<PassChoice> w = passes;
+        if (to_wil(w)) {
             passes = w;
             p->wil = true;
+        }
+    }
+    // The worker-interleaved plan with its tree fused into the first pass
+    // (MODE 11, k_pass wil_tree_to_lds): a tile of J adjacent line indices x
+    // all P workers loads each position's P leaves once -- J esz-byte leaf
+    // rows, 256 B at the default J -- and evaluates every worker's tree there,
+    // so the tree launch (N read + N written) and the first pass's re-read of
+    // its output are gone.  The first radix is what that tile leaves (8192 /
+    // (J P): 64 at fp64 P = 8), the rest of the local FFT is planned as
+    // usual.  PIFFT_WIL_FUSE=0: the separate tree launch (tuning, tests).
+    uint32_t wil_fused_c = 0;
+    if (p->wil && env_int("PIFFT_WIL_FUSE", 1)) {
+        const int J = env_int("PIFFT_WIL_FUSE_J", p->prec == 64 ? 16 : 32);
+        const int C1 = J << p->lp;
+        const int R1 = C1 > 0 ? tile_elems(p->prec) / C1 : 0;
+        const int nts1 = pick_nts(2 * ntrans * p->m * esz);
+        std::vector<PassChoice> rest;
+        const uint64_t m2 = R1 > 0 ? p->m / (uint64_t)R1 : 0;
+        bool ok = R1 >= 16 && (uint64_t)R1 < p->m && m2 >= (uint64_t)J && find_pass(p->prec, R1, C1, 11, nts1, p->lp) &&
+                  plan_passes(m2, p->prec, ntrans * (uint64_t)R1, rest, 0, false, false) == 0;
+        // (worker-interleaved passes exist up to R = 2048: a longer single
+        // remainder becomes two balanced passes)
+        if (ok && rest.size() == 1 && rest[0].R > 2048) {
+            const int l = ilog2u(m2);
+            rest = {PassChoice{1 << ((l + 1) / 2), 0, 2, rest[0].nts}, PassChoice{1 << (l / 2), 0, 2, rest[0].nts}};
+        }
+        if (ok && to_wil(rest)) {
+            passes.clear();
+            passes.push_back({R1, C1, 11, nts1});
+            for (const auto& pc : rest) passes.push_back(pc);
+            wil_fused_c = (uint32_t)C1;
         }
     }
     if (p->bitrev && !passes.empty()) {
@@ -759,7 +793,18 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const PassKernel* fused = nullptr;
     if (may_fuse && passes.size() > 1)
         fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp, passes[0].vpt);
+    if (wil_fused_c) fused = find_pass(p->prec, passes[0].R, passes[0].C, 11, passes[0].nts, p->lp);
     p->fused_tree = fused != nullptr;
+
+    // the worker-interleaved plan's tree twiddles (its k_tree_wil launch or
+    // its fused first pass): factored from 2^21 values up (wil_factored)
+    TreeTw wtw = ttw;
+    if (wil_factored) {
+        wtw.direct = nullptr;
+        wtw.lo = twp(tree2.lo);
+        wtw.hi = twp(tree2.hi);
+        wtw.h = tree2.h;
+    }
 
     // --- chain: [tree] [passes] [interleave] ---
     std::vector<Elem> chain;
@@ -819,12 +864,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
                                           (const void*)&k_tree_wil<float, 3>, (const void*)&k_tree_wil<float, 4>};
             Step& t = e.steps.back();
             t.fn = p->prec == 64 ? tw64[p->lp] : tw32[p->lp];
-            if (wil_factored) {
-                t.ta.tw.direct = nullptr;
-                t.ta.tw.lo = twp(tree2.lo);
-                t.ta.tw.hi = twp(tree2.hi);
-                t.ta.tw.h = tree2.h;
-            }
+            t.ta.tw = wtw;
             t.ta.out_bstride = p->n;
             t.lds = (size_t)tree_wil_pad(256u << p->lp) * esz;
             if (t.lds > 65536 && !dry) (void)hipFuncSetAttribute(t.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)t.lds);
@@ -857,7 +897,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         s.pa.tw_h = pass2.h;
         s.pa.in_bstride = (i == 0 && (!need_tree || fuse_here)) ? p->n : M;
         if (fuse_here) {
-            s.pa.tree = ttw;
+            s.pa.tree = p->wil ? wtw : ttw;
             s.pa.worker = p->q0;
             s.pa.log_nq = (uint32_t)ilog2u(p->nq);
         }
@@ -885,8 +925,9 @@ int build_plan(pifft_plan* p, bool dry = false) {
                                                              (unsigned long long)(wgs * k->nt));
         s.grid = dim3((unsigned)wgs);
         s.lds = (size_t)k->lds_bytes;
-        // (a fused pass reads every leaf of its worker's transform: N per worker)
-        s.bytes = !fuse_here ? 2 * ntrans * M * esz : (uint64_t)p->batch * p->nq * (p->n + M) * esz;
+        // (a one-worker fused pass reads every leaf of its worker's transform:
+        // N per worker; the all-worker one, MODE 11, each leaf once)
+        s.bytes = (!fuse_here || p->wil) ? 2 * ntrans * M * esz : (uint64_t)p->batch * p->nq * (p->n + M) * esz;
         if (s.lds > 65536 && !dry)
             (void)hipFuncSetAttribute(k->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
         if (i < 8) {

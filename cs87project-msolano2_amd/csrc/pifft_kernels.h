@@ -535,10 +535,19 @@ struct LdsPick {
 #include "pifft_lds_layouts.inc"
 #endif
 
-// dynamic LDS bytes of a k_pass instance (0 for a single-stage sub-FFT)
+// The stage maps (Stage) and LDS layout (LdsPick) a pass MODE uses: its
+// low two bits, except MODE 11 (the all-worker tree fused into the first
+// worker-interleaved pass), whose stages are those of a MODE 10 pass -- lanes
+// across lines on both strided sides.
+constexpr int stage_mode(int mode) { return ((mode & 3) == 3 && (mode & 8)) ? 2 : (mode & 3); }
+
+// dynamic LDS bytes of a k_pass instance (0 for a single-stage sub-FFT; MODE
+// 11 always exchanges: the tree's values reach the first stage through LDS)
 template <typename T, int R, int C, int MODE, int VPT>
 constexpr int pass_lds_bytes() {
-    return PassShape<R, VPT>::NSTG > 1 ? C * LdsPick<T, R, C, MODE & 3, VPT>::value.ls * (int)sizeof(T) : 0;
+    return (PassShape<R, VPT>::NSTG > 1 || MODE == 11)
+               ? C * LdsPick<T, R, C, stage_mode(MODE), VPT>::value.ls * (int)sizeof(T)
+               : 0;
 }
 
 // v[k] *= w^k (0 < k < q), w^k = w^(k - lowbit k) * w^(lowbit k), anchors
@@ -714,6 +723,72 @@ constexpr int pre_count() {
     return pre_offset<R, C, BM, VPT, PassShape<R, VPT>::NSTG>();
 }
 
+// MODE 11 = 3 | 8: the tree of ALL P = 2^LP workers fused into the first
+// worker-interleaved pass (an all-worker natural-order plan, PassArgs::wil =
+// LP).  The tile's C = J P launch lines are J adjacent line indices j times
+// the P workers (L = (j << LP) + q), so its C R inputs z_q[j + r M/R] come from
+// exactly J R P leaves x[j + r M/R + m M]: each position's P leaves are loaded
+// once (J adjacent j per leaf row: J esz-byte segments, 256 B at the
+// planner's J), the full radix-2 tree (tree_levels, every branch, the
+// reference's operation order) gives every worker's value there, and one LDS
+// transpose per component hands them to the pass's first stage (lanes across
+// lines, as MODE 10).  Replaces the all-worker tree launch (k_tree_wil),
+// which wrote the N tree values and had the first pass read them back.
+template <typename T, int R, int C, int LP, int VPT, int NTS>
+__device__ __forceinline__ void wil_tree_to_lds(const PassArgs& a, T* lds, cx<T>* v, int tid, uint64_t tile) {
+    using C2 = cx<T>;
+    using Sh = PassShape<R, VPT>;
+    using St = Stage<R, C, 2, 0, VPT>;
+    constexpr int P = 1 << LP, J = C / P;
+    constexpr int NT = PassCfg<R, C, VPT>::NT;
+    constexpr int PPT = Sh::Q / P;  // tree positions per thread
+    static_assert(C % P == 0 && Sh::Q % P == 0 && PPT * P * NT == C * R, "MODE 11 tile: J P lines, Q / P positions");
+    constexpr LdsLayout LL = LdsPick<T, R, C, 2, VPT>::value;
+    const uint32_t log_lb = a.log_lb;
+    const uint32_t lbi = log_lb + (uint32_t)LP;
+    const uint32_t log_m = log_lb + (uint32_t)Sh::LOGR;  // leaf stride M
+    const uint64_t line0 = tile * C;                    // (C divides a transform's lines: no partial tile)
+    const uint64_t bt = line0 >> lbi;
+    const uint64_t j0 = (line0 & ((1ull << lbi) - 1)) >> LP;
+    const C2* __restrict__ x = static_cast<const C2*>(a.in) + bt * a.in_bstride;
+    C2 w[PPT][P];
+#pragma unroll
+    for (int u = 0; u < PPT; u++) {  // every leaf load issued before any use
+        const int p = tid + u * NT;  // position: J adjacent j (lanes), then r
+        const uint64_t i = j0 + (uint64_t)(p % J) + ((uint64_t)(p / J) << log_lb);
+#pragma unroll
+        for (int m = 0; m < P; m++) w[u][m] = ld_stream<nt_loads(NTS)>(x + i + ((uint64_t)m << log_m));
+    }
+#pragma unroll
+    for (int u = 0; u < PPT; u++) {
+        const int p = tid + u * NT;
+        const uint64_t i = j0 + (uint64_t)(p % J) + ((uint64_t)(p / J) << log_lb);
+        tree_levels<T, LP>(w[u], a.tree, i, log_m, 0, 0, 0, 0, P);  // w[u][m] = z_m[i]
+    }
+#pragma unroll
+    for (int comp = 0; comp < 2; comp++) {
+        if (comp) __syncthreads();  // the first component's reads are done
+#pragma unroll
+        for (int u = 0; u < PPT; u++) {
+            const int p = tid + u * NT, jl = p % J, r = p / J;
+#pragma unroll
+            for (int m = 0; m < P; m++) lds[lds_at(LL, jl * P + m, r)] = comp ? w[u][m].im : w[u][m].re;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < St::U; u++) {
+            int c, b;
+            St::map(tid, u, c, b);
+#pragma unroll
+            for (int k = 0; k < St::q; k++) {
+                const T y = lds[lds_at(LL, c, b + k * St::NB)];
+                if (comp) v[u * St::q + k].im = y; else v[u * St::q + k].re = y;
+            }
+        }
+    }
+    __syncthreads();  // every read done before the first stage's exchange writes LDS
+}
+
 #ifndef PIFFT_SERIAL_BFLY
 #define PIFFT_SERIAL_BFLY 1
 #endif
@@ -729,10 +804,11 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     constexpr int BM = MODE & 3;
     constexpr bool BREV = (MODE & 4) != 0;
     constexpr bool WIL = (MODE & 8) != 0;  // worker-interleaved layout (PassArgs::wil)
-    using St = Stage<R, C, BM, S, VPT>;
+    constexpr int SM = stage_mode(MODE);   // the stage maps' mode (MODE 11: MODE 10's)
+    using St = Stage<R, C, SM, S, VPT>;
     using Sh = PassShape<R, VPT>;
     constexpr int q = St::q, U = St::U, NB = St::NB, ns = St::ns;
-    constexpr LdsLayout LL = LdsPick<T, R, C, BM, VPT>::value;
+    constexpr LdsLayout LL = LdsPick<T, R, C, SM, VPT>::value;
     // Several butterflies per thread (VPT 32): one after the other, each with
     // its own twiddles, loads and stores -- scheduling barriers keep the
     // compiler from interleaving their temporaries and hoisting their
@@ -776,7 +852,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             tw_pre[4 * u + 3] = thi[e1 >> a.tw_h];
         }
     }
-    if constexpr (St::first) {
+    if constexpr (St::first && BM == 3 && WIL) {
+        // ---- MODE 11: every worker's tree, then the first stage's inputs via LDS ----
+        wil_tree_to_lds<T, R, C, LP, VPT, NTS>(a, lds, v, tid, tile);
+    } else if constexpr (St::first) {
         // ---- inputs straight from HBM (all loads issued before any use) ----
         const C2* __restrict__ in = static_cast<const C2*>(a.in);
 #pragma unroll
@@ -967,12 +1046,12 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
                 }
             }
         }
-    } else if constexpr (Stage<R, C, BM, S + 1, VPT>::perm) {
+    } else if constexpr (Stage<R, C, SM, S + 1, VPT>::perm) {
         // ---- exchange with the last stage across lanes (Stage::perm) ----
         // quadruple g: row m, register 4g+j holds element 256 m + 16 (4g+j) + i;
         // afterwards it holds element 256 j + 16 (4g+m) + i (input j of
         // butterfly 64 g + 16 m + i)
-        if constexpr (Stage<R, C, BM, S + 1, VPT>::q == 4) {
+        if constexpr (Stage<R, C, SM, S + 1, VPT>::q == 4) {
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 pl_swap<32>(v[4 * g + 0], v[4 * g + 2]);
@@ -987,10 +1066,12 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile, twp);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
-        using Nx = Stage<R, C, BM, S + 1, VPT>;
+        using Nx = Stage<R, C, SM, S + 1, VPT>;
 #pragma unroll
         for (int comp = 0; comp < 2; comp++) {
-            // (the tile's first LDS store has no earlier reader to wait for)
+            // (the tile's first LDS store has no earlier reader to wait for;
+            // MODE 11's first stage has just read its inputs from LDS and
+            // waited for every thread's reads)
             if (S > 0 || comp > 0) lds_handoff<Nx::wave_private>();
             const int tidc = tid;
 #pragma unroll

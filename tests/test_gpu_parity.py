@@ -783,6 +783,7 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
     # reference-formula table -- the slice-major plan's -- the arithmetic is the
     # slice-major plan's, bit for bit)
     monkeypatch.setenv("PIFFT_WIL_TREE_DIRECT", "1")
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")  # (the tree as its own launch, as the slice-major plan's)
     wil = pifft.Plan(n, P, batch, PREC[suf])
     assert wil.describe()["worker_interleaved"] and "interleave" not in wil.describe()["launch_kind"]
     assert set(wil.describe()["vpt"]) == {16}
@@ -799,6 +800,34 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
     for bt in range(batch):
         assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
 
+
+
+@pytest.mark.parametrize("suf,logn,P,batch,j", [("f64", 20, 8, 1, 0), ("f64", 20, 8, 1, 8), ("f32", 20, 8, 1, 0),
+                                                ("f64", 18, 4, 2, 0), ("f64", 16, 2, 3, 0), ("f64", 22, 16, 1, 0),
+                                                ("f32", 22, 16, 2, 0), ("f64", 21, 8, 1, 0), ("f32", 17, 2, 1, 16),
+                                                ("f64", 24, 8, 1, 0), ("f32", 23, 4, 1, 0), ("f64", 19, 16, 1, 8)])
+def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
+    """All-worker natural-order plans with every worker's tree fused into the
+    first worker-interleaved pass (MODE 11: each position's P leaves loaded
+    once, the full radix-2 tree, an LDS transpose into the pass): against the
+    oracle (tolerance + per bin) and against the same plan with the tree as
+    its own launch (PIFFT_WIL_FUSE=0).  j: the tile's adjacent line indices
+    (PIFFT_WIL_FUSE_J; 0 = the planner's)."""
+    n = 1 << logn
+    x = oracle.generate(n * batch, DT[suf], seed=logn * 5 + P + j)
+    if j:
+        monkeypatch.setenv("PIFFT_WIL_FUSE_J", str(j))
+    fused = pifft.Plan(n, P, batch, PREC[suf])
+    d = fused.describe()
+    assert d["worker_interleaved"] and d["launch_kind"][0] == "tree+pass" and d["launch_mode"][0] == 11, d
+    assert "tree" not in d["launch_kind"] and "interleave" not in d["launch_kind"]
+    got = run(fused, x).reshape(batch, n)
+    for bt in range(batch):
+        assert_bins_close(got[bt], oracle.fft(x[bt * n:(bt + 1) * n], P=1, nthreads=8), suf, n)
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")
+    sep = pifft.Plan(n, P, batch, PREC[suf])
+    assert sep.describe()["launch_kind"][0] == "tree"
+    assert rel_l2(run(sep, x), got.reshape(-1)) <= tol(suf, n)
 
 
 # ------------------------------------------------ the final exchange (8e) ---

@@ -5,7 +5,8 @@ PKV(..., VPT) names the values per thread (8 or 32) explicitly.
 
 Rules: NT = C*R/VPT threads (VPT = 16 values per thread) <= 1024; LDS = C*(R + R/16 + 1)*sizeof(T)
 <= 160 KiB.  MODE 0 single pass (any C); MODE 1/2 strided passes (C >= 4);
-MODE 10 = MODE 2 on the worker-interleaved layout (all-worker plans).
+MODE 10 = MODE 2 on the worker-interleaved layout (all-worker plans);
+MODE 11 = its first pass with every worker's tree fused in.
 MODE 3 = MODE 1 with the tree fused in, LP = log2 P in 1..4, at the planner's
 tile (8192 elements, both precisions) and C = 4.  MODE 4 / 6 = MODE 0 / 2
 storing in bit-reversed order (the last pass of a PIFFT_OUT_BITREV plan), for
@@ -42,9 +43,13 @@ for T, prec, esz, tile, vpt in (("double", 64, 8, 8192, 16), ("float", 32, 4, 16
                     if C <= max(4, tile // R):
                         items.append(f"PK({T}, {prec}, {R}, {C}, 6, {nts}, 0),")
                         # MODE 10 = 2 | 8: the worker-interleaved layout of
-                        # all-worker plans (multi-pass local FFTs: R <= 1024)
-                        if R <= 1024:
+                        # all-worker plans (multi-pass local FFTs: R <= 1024;
+                        # 2048 at C = 4 for the pass after a fused tree pass,
+                        # MODE 11, e.g. config 2's 64 x 2048)
+                        if R <= 1024 or (R == 2048 and C == 4):
                             items.append(f"PK({T}, {prec}, {R}, {C}, 10, {nts}, 0),")
+                    if R == 2048 and C == 8:  # (its 8-line twin: a row of all 8 workers)
+                        items.append(f"PK({T}, {prec}, {R}, {C}, 10, {nts}, 0),")
                 # the planner's first-pass tile (tile_elems(): 8192 values for both precisions)
                 # (and at half that C for R <= 256: the planner halves C to keep >= 512
                 # workgroups on small local sizes, e.g. 2^21 = 128 x 128 x 128)
@@ -100,6 +105,20 @@ for R in (256, 512):
     for C in (4, 8):
         for nts in (0, 1):
             items.append(f"PKV(double, 64, {R}, {C}, 2, {nts}, 0, 8),")
+# MODE 11 = 3 | 8: the tree of all P workers fused into the first
+# worker-interleaved pass (round 5).  A tile is J adjacent line indices x the P
+# workers (C = J P lines) at the 8192-value tile (R = 8192 / C): J = 16 fp64 /
+# 32 fp32 (256-B leaf rows, the planner's default) and half that
+# (PIFFT_WIL_FUSE_J, tuning), P = 2..16.
+for T, prec, js in (("double", 64, (16, 8)), ("float", 32, (32, 16))):
+    for J in js:
+        for lp in (1, 2, 3, 4):
+            C = J << lp
+            R = 8192 // C
+            if R < 16:
+                continue
+            for nts in (0, 1):
+                items.append(f"PK({T}, {prec}, {R}, {C}, 11, {nts}, {lp}),")
 # (config 2's slice with its fused tree pass at C = 2 -- 128 workgroups
 # gathering leaves, 32-B leaf segments: +0.7 % on the slice, 0 to +2.4 % on
 # neighbouring slices, within run-to-run noise; round 4,
