@@ -110,7 +110,7 @@ for R in (256, 512):
 # workers (C = J P lines) at the 8192-value tile (R = 8192 / C): J = 16 fp64 /
 # 32 fp32 (256-B leaf rows, the planner's default) and half that
 # (PIFFT_WIL_FUSE_J, tuning), P = 2..16.
-for T, prec, js in (("double", 64, (16, 8)), ("float", 32, (32, 16))):
+for T, prec, js in (("double", 64, (16, 8, 4)), ("float", 32, (32, 16, 8))):
     for J in js:
         for lp in (1, 2, 3, 4):
             C = J << lp
