@@ -660,16 +660,30 @@ int build_plan(pifft_plan* p, bool dry = false) {
     }
     // The worker-interleaved plan with its tree fused into the first pass
     // (MODE 11, k_pass wil_tree_to_lds): a tile of J adjacent line indices x
-    // all P workers loads each position's P leaves once -- J esz-byte leaf
-    // rows, 256 B at the default J -- and evaluates every worker's tree there,
-    // so the tree launch (N read + N written) and the first pass's re-read of
-    // its output are gone.  The first radix is what that tile leaves (8192 /
-    // (J P): 64 at fp64 P = 8), the rest of the local FFT is planned as
-    // usual.  PIFFT_WIL_FUSE=0: the separate tree launch (tuning, tests).
+    // all P workers loads each position's P leaves once (J esz-byte leaf
+    // rows) and evaluates every worker's tree there, so the tree launch (N
+    // read + N written) and the first pass's re-read of its output are gone.
+    // The first radix is what that tile leaves (8192 / (J P)), the rest of
+    // the local FFT is planned as usual.  J by measurement (round 5,
+    // profiles/r05m_wil_fuse_j.log, the separate tree launch in brackets):
+    //   fp64, J = 8: config 2 (2^20 P = 8) 26 us (29), 2^20 P = 4 23 (31),
+    //     P = 2 25 (31), 2^24 P = 8 310 (381), 2^26 P = 4 1.18 ms (1.50),
+    //     2^28 P = 8 4.98 ms (6.31), P = 16 5.84 (6.13); but P = 16 below
+    //     256 MiB ties or loses (2^20: 28-45 vs 26 us) -> separate there;
+    //     J = 16 (256-B leaf rows, first radix 64 at P = 8) loses on the
+    //     remaining passes it leaves (a 1024 / 2048 pass at 8 lines);
+    //   fp32: J = 8 up to 32 MiB (2^20 P = 8 20 vs 24 us), J = 16 up to
+    //     1 GiB (2^24 P = 8 165 vs 208 us); 2^28 P = 8 keeps the separate tree
+    //     (3.26 vs 3.39-3.51 ms: its remaining passes at 8-B values get
+    //     128-B rows).
+    // PIFFT_WIL_FUSE=0: the separate tree launch; PIFFT_WIL_FUSE_J: J (tuning, tests).
     uint32_t wil_fused_c = 0;
     if (p->wil && env_int("PIFFT_WIL_FUSE", 1)) {
-        const int J = env_int("PIFFT_WIL_FUSE_J", p->prec == 64 ? 16 : 32);
-        const int C1 = J << p->lp;
+        const uint64_t data = (uint64_t)p->batch * p->n * esz;
+        const int jdef = p->prec == 64 ? ((p->lp <= 3 || data >= (256ull << 20)) ? 8 : 0)
+                                       : (data <= (32ull << 20) ? 8 : data <= (1ull << 30) ? 16 : 0);
+        const int J = env_int("PIFFT_WIL_FUSE_J", jdef);
+        const int C1 = J > 0 ? J << p->lp : 0;
         const int R1 = C1 > 0 ? tile_elems(p->prec) / C1 : 0;
         const int nts1 = pick_nts(2 * ntrans * p->m * esz);
         std::vector<PassChoice> rest;

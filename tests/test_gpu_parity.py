@@ -802,10 +802,11 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
 
 
 
-@pytest.mark.parametrize("suf,logn,P,batch,j", [("f64", 20, 8, 1, 0), ("f64", 20, 8, 1, 8), ("f32", 20, 8, 1, 0),
-                                                ("f64", 18, 4, 2, 0), ("f64", 16, 2, 3, 0), ("f64", 22, 16, 1, 0),
-                                                ("f32", 22, 16, 2, 0), ("f64", 21, 8, 1, 0), ("f32", 17, 2, 1, 16),
-                                                ("f64", 24, 8, 1, 0), ("f32", 23, 4, 1, 0), ("f64", 19, 16, 1, 8)])
+@pytest.mark.parametrize("suf,logn,P,batch,j", [("f64", 20, 8, 1, 0), ("f64", 20, 8, 1, 16), ("f32", 20, 8, 1, 0),
+                                                ("f64", 18, 4, 2, 0), ("f64", 16, 2, 3, 0), ("f64", 22, 16, 1, 4),
+                                                ("f32", 22, 16, 2, 0), ("f64", 21, 8, 1, 4), ("f32", 17, 2, 1, 32),
+                                                ("f64", 24, 8, 1, 0), ("f32", 23, 4, 1, 0), ("f64", 19, 16, 1, 8),
+                                                ("f32", 20, 8, 1, 16), ("f64", 20, 2, 1, 0)])
 def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
     """All-worker natural-order plans with every worker's tree fused into the
     first worker-interleaved pass (MODE 11: each position's P leaves loaded

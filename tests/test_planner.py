@@ -15,11 +15,34 @@ def test_config1_2e20_fp64_one_worker():
     assert d["radix"] == [1024, 1024]
 
 
-def test_config2_2e20_fp64_eight_workers_one_gpu():
+def test_config2_2e20_fp64_eight_workers_one_gpu(monkeypatch):
     d = pifft.dry_run(1 << 20, 8, 1, F64)
-    # the last pass stores natural order itself (16 MiB output): no interleave launch
-    assert d["launch_kind"] == ["tree", "pass", "pass"]
+    # the worker-interleaved layout with every worker's tree fused into the
+    # first pass (MODE 11: 8 adjacent line indices x 8 workers, first radix
+    # 128), the last pass storing natural order itself: two launches
+    assert d["worker_interleaved"] and d["launch_kind"] == ["tree+pass", "pass"]
+    assert d["launch_mode"] == [11, 10] and d["radix"] == [128, 1024] and d["lines"] == [64, 8]
     assert d["local_n"] == 1 << 17 and d["out_elems"] == 1 << 20
+    assert d["launch_bytes"] == [2 * (1 << 20) * 16] * 2  # each leaf read once, every value written once
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")  # the tree as its own launch
+    assert pifft.dry_run(1 << 20, 8, 1, F64)["launch_kind"] == ["tree", "pass", "pass"]
+
+
+def test_fused_all_worker_rule():
+    """Which all-worker plans fuse the tree into the first pass (MODE 11) and
+    at which J (the tile's adjacent line indices: first radix 8192 / (J P)) --
+    the planner's measured rule (profiles/r05m_wil_fuse_j.log)."""
+    def first(n, P, prec, b=1):
+        d = pifft.dry_run(n, P, b, prec)
+        return d["launch_mode"][0], d["radix"][0], d["lines"][0]
+    assert first(1 << 20, 8, F64) == (11, 128, 64)     # fp64 P <= 8: J = 8
+    assert first(1 << 28, 8, F64) == (11, 128, 64)
+    assert first(1 << 20, 2, F64) == (11, 512, 16)
+    assert first(1 << 22, 16, F64)[0] == 0               # fp64 P = 16 below 256 MiB: the tree launch
+    assert first(1 << 28, 16, F64) == (11, 64, 128)     # ... and from 256 MiB fused
+    assert first(1 << 20, 8, F32) == (11, 128, 64)      # fp32 up to 32 MiB: J = 8
+    assert first(1 << 24, 8, F32) == (11, 64, 128)      # up to 1 GiB: J = 16
+    assert first(1 << 28, 8, F32)[0] == 0                # beyond: the tree launch
 
 
 def test_natural_store_rule(monkeypatch):
@@ -189,7 +212,7 @@ def test_worker_interleaved_layout(monkeypatch):
     slice-major layout.  Single-pass local FFTs, P > 16 and worker ranges keep
     the slice-major layout."""
     d = pifft.dry_run(1 << 20, 8, 1, F64)
-    assert d["worker_interleaved"] and not d["natural_store"] and d["launch_kind"] == ["tree", "pass", "pass"]
+    assert d["worker_interleaved"] and not d["natural_store"] and d["launch_kind"] == ["tree+pass", "pass"]
     big = pifft.dry_run(1 << 28, 8, 1, F64)
     assert big["worker_interleaved"] and "interleave" not in big["launch_kind"]
     assert not pifft.dry_run(1 << 16, 8, 1, F64)["worker_interleaved"]          # single-pass local FFT
@@ -215,11 +238,14 @@ def test_position_model_off_restores_bandwidth_model(monkeypatch):
     assert pifft.dry_run(1 << 20, 1, 1, F64)["radix"] == small
 
 
-def test_position_model_not_for_worker_interleaved_plans():
+def test_position_model_not_for_worker_interleaved_plans(monkeypatch):
     """All-worker plans in the worker-interleaved layout keep the segment-width
     model's order (the narrow pass last measured 1-14 % slower there,
     profiles/r03_pos_model_shapes.log); one-worker plans of the same local
-    size put it last."""
+    size put it last.  (The tree as its own launch: with it fused, MODE 11,
+    the first radix is the fused tile's and the rest is planned after it.)"""
+    assert pifft.dry_run(1 << 29, 2, 1, F64)["radix"] == [512, 1024, 512]
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")
     wil = pifft.dry_run(1 << 29, 2, 1, F64)
     assert wil["worker_interleaved"] and wil["radix"] == [1024, 512, 512]
     assert pifft.dry_run(1 << 28, 1, 1, F64)["radix"] == [512, 512, 1024]
@@ -229,7 +255,9 @@ def test_position_model_not_for_worker_interleaved_plans():
 STRAY = {"PIFFT_ORDER": "1", "PIFFT_PASSES": "4", "PIFFT_RADIX_LOGS": "10,10,8", "PIFFT_NT": "0",
          "PIFFT_WORKER_IL": "0", "PIFFT_POS_MODEL": "0", "PIFFT_VPT32": "0", "PIFFT_W_PAD": "0",
          "PIFFT_TILE64": "4096", "PIFFT_LAST_C": "16", "PIFFT_FUSE_TREE": "0", "PIFFT_ILV": "1",
-         "PIFFT_SINGLE_TILE32": "8192", "PIFFT_LAST_VPT": "16", "PIFFT_FUSED_VPT": "16", "PIFFT_WIL_VPT": "16"}
+         "PIFFT_SINGLE_TILE32": "8192", "PIFFT_LAST_VPT": "16", "PIFFT_FUSED_VPT": "16", "PIFFT_WIL_VPT": "16",
+         "PIFFT_WIL_FUSE": "0", "PIFFT_WIL_FUSE_J": "16", "PIFFT_WIL_TREE_DIRECT": "1", "PIFFT_WIL_TREE_MIN_LOG": "0",
+         "PIFFT_PERMLANE": "0", "PIFFT_FAULT": "broadcast"}
 
 
 @pytest.mark.parametrize("shape", [(1 << 28, 1, 1, F64, 0, 1, 0), (1 << 28, 1, 1, F32, 0, 1, 0),
@@ -252,7 +280,7 @@ def test_stray_tuning_variables_are_ignored(shape, monkeypatch):
     assert pifft.dry_run(n, P, b, prec, first=first, count=count, flags=flags) != want
 
 
-def test_small_slices_run_the_fused_pass_at_8_values_per_thread():
+def test_small_slices_run_the_fused_pass_at_8_values_per_thread(monkeypatch):
     """Round 4 (profiles/r04d_fused_vpt8.log): a one-worker slice's fused tree
     pass runs at 8 values per thread when it has R <= 512 points and at most
     128 workgroups (config 2's slice: 14.05 -> 12.66 us); R = 1024 and larger
@@ -269,5 +297,9 @@ def test_small_slices_run_the_fused_pass_at_8_values_per_thread():
     assert pifft.dry_run(1 << 17, 1, 1, F64)["vpt"] == [16, 8]                    # P = 1: the last pass only
     assert pifft.dry_run(1 << 20, 1, 1, F64)["vpt"] == [16, 16]                   # config 1 (R = 1024)
     assert pifft.dry_run(1 << 17, 1, 1, F32)["vpt"] == [16, 16]                   # fp64 only
+    # config 2: the fused all-worker pass (MODE 11) and a 1024-point pass at 16; with the tree as
+    # its own launch the worker-interleaved passes run at 8
+    assert pifft.dry_run(1 << 20, 8, 1, F64)["vpt"] == [16, 16]
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")
     assert pifft.dry_run(1 << 20, 8, 1, F64)["vpt"] == [8, 8]                     # config 2 (worker-interleaved)
     assert pifft.dry_run(1 << 28, 8, 1, F64)["vpt"] == [16, 16, 16]
