@@ -676,9 +676,10 @@ int build_plan(pifft_plan* p, bool dry = false) {
     //     1 GiB (2^24 P = 8 165 vs 208 us); 2^28 P = 8 keeps the separate tree
     //     (3.26 vs 3.39-3.51 ms: its remaining passes at 8-B values get
     //     128-B rows).
-    // PIFFT_WIL_FUSE=0: the separate tree launch; PIFFT_WIL_FUSE_J: J (tuning, tests).
+    // PIFFT_SEPARATE_TREE (CLI -u) or PIFFT_WIL_FUSE=0: the separate tree
+    // launch; PIFFT_WIL_FUSE_J: J (tuning, tests).
     uint32_t wil_fused_c = 0;
-    if (p->wil && env_int("PIFFT_WIL_FUSE", 1)) {
+    if (p->wil && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
         const uint64_t data = (uint64_t)p->batch * p->n * esz;
         const int jdef = p->prec == 64 ? ((p->lp <= 3 || data >= (256ull << 20)) ? 8 : 0)
                                        : (data <= (32ull << 20) ? 8 : data <= (1ull << 30) ? 16 : 0);

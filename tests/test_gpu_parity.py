@@ -288,8 +288,9 @@ def test_host_boundary_and_group():
     assert_bins_close(out2, want, "f64", n)
 
 
-def test_timed_execution_reports_every_launch():
+def test_timed_execution_reports_every_launch(monkeypatch):
     n = 1 << 20
+    monkeypatch.setenv("PIFFT_WIL_FUSE", "0")  # (the three-launch form: tree + two passes)
     plan = pifft.Plan(n, 8, 1, pifft.F64)
     d = plan.describe()
     x = torch.empty(n, dtype=torch.complex128, device="cuda")
@@ -589,14 +590,16 @@ def test_cli_separate_tree_stage_columns(tmp_path):
     """CLI -u (PIFFT_SEPARATE_TREE): the tree stays its own launch, so the TSV's
     stage-1 column is the funnel alone (the column analyze-results.R:56 fits
     on n(p-1)/p); without it a one-worker-per-GPU plan fuses the tree into the
-    first pass (stage 1 = tree + first pass).  Same output either way."""
+    first pass (stage 1 = tree + first pass), and an all-worker plan too
+    (MODE 11, whose first radix then differs).  The same transform either
+    way."""
     import subprocess
     cli = pifft.CLI_PATH
     n, P = 1 << 20, 8
     outs = {}
     for flag in ([], ["-u"]):
-        # (one GPU holds all 8 workers here: unfused either way; the stage
-        # split of a one-worker plan is checked through the ABI below)
+        # (one GPU holds all 8 workers here; the stage split of a one-worker
+        # plan is checked through the ABI below)
         dump = str(tmp_path / f"out{len(flag)}.bin")
         r = subprocess.run([cli, "-n", str(n), "-p", str(P), "-o", "-f", "64", "-s", "3", "-w", dump] + flag,
                            capture_output=True, text=True, timeout=120)
@@ -604,7 +607,8 @@ def test_cli_separate_tree_stage_columns(tmp_path):
         cols = r.stdout.strip().splitlines()[-1].split("\t")
         assert len(cols) == 5 and float(cols[3]) > 0 and float(cols[4]) > 0
         outs[bool(flag)] = open(dump, "rb").read()
-    assert outs[True] == outs[False]
+    a, b = (np.frombuffer(outs[k], dtype=np.complex128) for k in (False, True))
+    assert rel_l2(a, b) <= 1e-12
     x = oracle.generate(n, np.complex128, seed=3)
     fused = pifft.Plan(n, P, 1, pifft.F64, first=0, count=1, device=0)
     sep = pifft.Plan(n, P, 1, pifft.F64, first=0, count=1, device=0, flags=pifft.OUT_SLICES | pifft.SEPARATE_TREE)
