@@ -966,6 +966,7 @@ def test_multi_gpu_error_paths_fail_cleanly(site, monkeypatch):
     for p, sl in zip(plans, slices):
         p.execute_device(d_in.data_ptr(), sl.data_ptr(), st)
     nat = torch.empty(n * batch, dtype=d_in.dtype, device="cuda")
+    torch.cuda.synchronize()  # (pifft_allgather: once the executions that produced the slices have completed)
     pifft.allgather(plans, [sl.data_ptr() for sl in slices], [nat.data_ptr()] + [None] * (P - 1))
     torch.cuda.synchronize()
     free0 = torch.cuda.mem_get_info(0)[0]
