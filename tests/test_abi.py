@@ -9,10 +9,20 @@ import pytest
 import pifft
 
 
-def test_library_is_built_for_gfx950():
+def test_library_is_built_for_gfx950(tmp_path):
+    """The fat binary's device bundles: gfx950 code objects only (stored
+    compressed, --offload-compress: listed through llvm-objdump, which
+    inflates them)."""
+    import shutil
+    import subprocess
     assert os.path.exists(pifft.LIB_PATH), "run __graft_entry__.build()"
-    blob = open(pifft.LIB_PATH, "rb").read()
-    assert b"gfx950" in blob
+    lib = tmp_path / "libpifft.so"  # (llvm-objdump extracts the bundles beside its input)
+    shutil.copy(pifft.LIB_PATH, lib)
+    r = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)], capture_output=True,
+                       text=True, timeout=120, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    targets = {ln.rsplit("--", 1)[-1] for ln in r.stdout.splitlines() if "hipv4-amdgcn-amd-amdhsa--" in ln}
+    assert targets == {"gfx950"}, r.stdout
 
 
 def test_exports_every_header_symbol():
