@@ -33,6 +33,13 @@ import sys
 
 TOL = 0.03
 BACK_TO_BACK_US = 2.0
+# Across two runs (the untraced line vs the traced run's kernel durations) a
+# kernel shorter than this is tracer-limited: rocprofv3 adds 0.1-1 us to each
+# small dispatch's own duration, by box (round 4 r04j: config 2's slice
+# +13.9 %; round 5 r05k/r05q +8-16 % on its 7-us kernel, while the traced
+# run's own line matches its trace to 0.04 %).  Such rows are printed and
+# marked, and kept out of the verdict; --same-run checks every row.
+TRACER_LIMITED_MS = 0.010
 
 
 def rooflines(line):
@@ -102,12 +109,16 @@ def main():
             continue
         frac_tr = rf["algorithmic_bytes"] / (ref * 1e-3) / 1e9 / rf["peak"]
         diff = rf["frac"] / frac_tr - 1.0
-        worst = max(worst, abs(diff))
-        ok = ok and abs(diff) <= TOL
         bench_ms = rf.get("mean_ms", rf["algorithmic_bytes"] / (rf["achieved"] * 1e9) * 1e3)
+        limited = not same_run and bench_ms < TRACER_LIMITED_MS
+        if not limited:
+            worst = max(worst, abs(diff))
+            ok = ok and abs(diff) <= TOL
         print(f"{key:10s} {bench_ms:10.5f} {ref:10.5f} {kern:10.5f} {st if st is not None else float('nan'):10.5f} "
-              f"{rf['frac']:7.4f} {frac_tr:8.4f} {diff:+7.2%}  {name}  ({count} dispatches, {how})")
-    print(f"worst |frac difference| {worst:.2%}: {'OK' if ok else 'FAIL'} (tolerance {TOL:.0%})")
+              f"{rf['frac']:7.4f} {frac_tr:8.4f} {diff:+7.2%}  {name}  ({count} dispatches, {how})"
+              + ("  [tracer-limited: < 10 us, not in the verdict]" if limited else ""))
+    print(f"worst |frac difference| {worst:.2%}: {'OK' if ok else 'FAIL'} (tolerance {TOL:.0%}"
+          + ("" if same_run else f"; kernels under {TRACER_LIMITED_MS * 1e3:.0f} us shown, not judged") + ")")
     return 0 if ok else 1
 
 
