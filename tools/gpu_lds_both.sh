@@ -1,4 +1,5 @@
 #!/bin/bash
+# Historical: PIFFT_LDS_BOTH_MAX was removed after this A/B; kept as the record of how its log was taken.
 # A/B of the both-components LDS exchange (PIFFT_LDS_BOTH_MAX) on the small
 # configs and C4: tools/mkvariant.sh builds, copied to abvar/.
 set -o pipefail

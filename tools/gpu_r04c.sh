@@ -1,4 +1,5 @@
 #!/bin/bash
+# Historical in part: PIFFT_STRIDED_VPT was removed after this session; at HEAD that sweep runs the default.
 # tools/gpu_r04c.sh -- round-4 session c: PMC traffic of the C4 / C4_f32 / C3
 # plans (tools/gpu_r04.sh stage p), then A/B sweeps of the fp32 2^28 last pass
 # (XCD tile grouping, streaming form, workspace row pad) and config 2's

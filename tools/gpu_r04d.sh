@@ -1,4 +1,5 @@
 #!/bin/bash
+# Historical in part: PIFFT_W_BLOCK / PIFFT_Y_BLOCK were removed after this session; at HEAD those legs run the default.
 # tools/gpu_r04d.sh -- round-4 session d: the fused tree pass at 8 values per
 # thread (PIFFT_FUSED_VPT=8) over the small one-worker slices whose fused
 # launch has few workgroups, and config 2's worker-interleaved passes at 8

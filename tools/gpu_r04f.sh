@@ -1,4 +1,5 @@
 #!/bin/bash
+# Historical: the -DPIFFT_SINGLE_WPE variant build was removed after this session.
 # tools/gpu_r04f.sh -- round-4 session f: config 3's single pass built for 8
 # waves per SIMD (abvar2/wpe8.so, -DPIFFT_SINGLE_WPE=8: 64 VGPRs, 8 workgroups
 # per CU instead of 7 for its 16 per CU) vs the default build, then the HEAD

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Historical: PIFFT_FUSED_C was removed after this session; at HEAD that leg runs the default.
 # tools/gpu_r04n.sh -- round-4 session n: config 2's slice with its fused tree
 # pass at C = 2 (128 workgroups gathering leaves; PIFFT_FUSED_C), parity
 # first, then A/B on the slice and its neighbours.

@@ -8,6 +8,8 @@ created (its W allocated) and timed (HIP events per pass, 8 steps x 2 reps,
 the faster rep) and its output checked bitwise against the first one.
 Nothing is freed, so every (W, y) pair is a new placement (the pass-2/3 time
 is a property of the pair: tools/probe_place.py).  A probe, not product.
+Historical in part: PIFFT_INPLACE_LAST was removed after round 2 (PIFFT_W_PAD
+remains).
 """
 import os
 import sys
