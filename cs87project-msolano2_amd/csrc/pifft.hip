@@ -676,20 +676,50 @@ int build_plan(pifft_plan* p, bool dry = false) {
     //     1 GiB (2^24 P = 8 165 vs 208 us); 2^28 P = 8 keeps the separate tree
     //     (3.26 vs 3.39-3.51 ms: its remaining passes at 8-B values get
     //     128-B rows).
+    // Two refinements for P <= 8 (round 5, profiles/r05s_*, r05t_*, r05u_*;
+    // every output checked against the default plan's):
+    //   - where the 8192-value tile leaves fewer than 256 workgroups (<= 2^20
+    //     values: 128), the tile is halved and J = 4, so every CU gets one:
+    //     config 2 26 -> 23 us, fp64 2^20 P = 4 23 -> 21, P = 2 25 -> 23,
+    //     2^19 P = 8 21 -> 18, 2^18 P = 8 16 -> 14; fp32 2^20 P = 2-8 -1 us;
+    //   - where J = 8 leaves a remainder the rest of the plan splits in two
+    //     passes (> 2048 points) and J = 4 leaves one pass: J = 4 (fp64 2^22
+    //     P = 2 / 4 / 8: 68 / 65 / 64 -> 54 / 51 / 50 us); fp32 at P = 8 from a
+    //     2048-point remainder on (2^21 27 -> 24 us, 2^22 51 -> 42).  (fp32 at
+    //     P <= 4 keeps J = 8: its J = 4 remainder passes run at 4 lines, 32-B
+    //     rows: 2^22 P = 4 50 -> 75 us.)
     // PIFFT_SEPARATE_TREE (CLI -u) or PIFFT_WIL_FUSE=0: the separate tree
-    // launch; PIFFT_WIL_FUSE_J: J (tuning, tests).
+    // launch; PIFFT_WIL_FUSE_J: J (then the tile stays 8192 unless
+    // PIFFT_WIL_FUSE_TILE says otherwise), PIFFT_WIL_FUSE_TILE: the tile
+    // (values), PIFFT_WIL_FUSE_VPT: values per thread (tuning, tests).
     uint32_t wil_fused_c = 0;
     if (p->wil && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
         const uint64_t data = (uint64_t)p->batch * p->n * esz;
         const int jdef = p->prec == 64 ? ((p->lp <= 3 || data >= (256ull << 20)) ? 8 : 0)
                                        : (data <= (32ull << 20) ? 8 : data <= (1ull << 30) ? 16 : 0);
-        const int J = env_int("PIFFT_WIL_FUSE_J", jdef);
+        int J = jdef, tile1 = tile_elems(p->prec);
+        if (jdef == 8 && p->lp <= 3) {
+            const uint64_t rest8 = p->m / (uint64_t)(tile1 / (8 << p->lp)), rest4 = rest8 / 2;
+            if ((uint64_t)p->batch * p->n / (uint64_t)tile1 < 256) {
+                tile1 /= 2;
+                J = 4;
+            } else if (rest8 > (p->prec == 64 ? 2048u : 1024u) && rest4 <= 2048 && (p->prec == 64 || p->lp == 3)) {
+                J = 4;
+            }
+        }
+        const int jenv = env_int("PIFFT_WIL_FUSE_J", -1);
+        if (jenv >= 0) {
+            J = jenv;
+            tile1 = tile_elems(p->prec);
+        }
+        tile1 = env_int("PIFFT_WIL_FUSE_TILE", tile1);
         const int C1 = J > 0 ? J << p->lp : 0;
-        const int R1 = C1 > 0 ? tile_elems(p->prec) / C1 : 0;
+        const int R1 = C1 > 0 ? tile1 / C1 : 0;
+        const int vpt1 = env_int("PIFFT_WIL_FUSE_VPT", 16);
         const int nts1 = pick_nts(2 * ntrans * p->m * esz);
         std::vector<PassChoice> rest;
         const uint64_t m2 = R1 > 0 ? p->m / (uint64_t)R1 : 0;
-        bool ok = R1 >= 16 && (uint64_t)R1 < p->m && m2 >= (uint64_t)J && find_pass(p->prec, R1, C1, 11, nts1, p->lp) &&
+        bool ok = R1 >= 16 && (uint64_t)R1 < p->m && m2 >= (uint64_t)J && find_pass(p->prec, R1, C1, 11, nts1, p->lp, vpt1) &&
                   plan_passes(m2, p->prec, ntrans * (uint64_t)R1, rest, 0, false, false) == 0;
         // (worker-interleaved passes exist up to R = 2048: a longer single
         // remainder becomes two balanced passes)
@@ -699,7 +729,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
         if (ok && to_wil(rest)) {
             passes.clear();
-            passes.push_back({R1, C1, 11, nts1});
+            passes.push_back({R1, C1, 11, nts1, vpt1});
             for (const auto& pc : rest) passes.push_back(pc);
             wil_fused_c = (uint32_t)C1;
         }
@@ -808,7 +838,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     const PassKernel* fused = nullptr;
     if (may_fuse && passes.size() > 1)
         fused = find_pass(p->prec, passes[0].R, passes[0].C, 3, passes[0].nts, p->lp, passes[0].vpt);
-    if (wil_fused_c) fused = find_pass(p->prec, passes[0].R, passes[0].C, 11, passes[0].nts, p->lp);
+    if (wil_fused_c) fused = find_pass(p->prec, passes[0].R, passes[0].C, 11, passes[0].nts, p->lp, passes[0].vpt);
     p->fused_tree = fused != nullptr;
 
     // the worker-interleaved plan's tree twiddles (its k_tree_wil launch or

@@ -810,14 +810,17 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
                                                 ("f64", 18, 4, 2, 0), ("f64", 16, 2, 3, 0), ("f64", 22, 16, 1, 4),
                                                 ("f32", 22, 16, 2, 0), ("f64", 21, 8, 1, 4), ("f32", 17, 2, 1, 32),
                                                 ("f64", 24, 8, 1, 0), ("f32", 23, 4, 1, 0), ("f64", 19, 16, 1, 8),
-                                                ("f32", 20, 8, 1, 16), ("f64", 20, 2, 1, 0)])
+                                                ("f32", 20, 8, 1, 16), ("f64", 20, 2, 1, 0), ("f64", 22, 4, 1, 0),
+                                                ("f64", 22, 8, 1, 0), ("f32", 21, 8, 1, 0), ("f32", 22, 8, 1, 0),
+                                                ("f64", 17, 4, 1, 0), ("f32", 18, 8, 2, 0)])
 def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
     """All-worker natural-order plans with every worker's tree fused into the
     first worker-interleaved pass (MODE 11: each position's P leaves loaded
     once, the full radix-2 tree, an LDS transpose into the pass): against the
     oracle (tolerance + per bin) and against the same plan with the tree as
     its own launch (PIFFT_WIL_FUSE=0).  j: the tile's adjacent line indices
-    (PIFFT_WIL_FUSE_J; 0 = the planner's)."""
+    (PIFFT_WIL_FUSE_J; 0 = the planner's: the 4096-value tile at J = 4 up to
+    2^20 values, J = 4 where J = 8 would split the remainder, else J = 8)."""
     n = 1 << logn
     x = oracle.generate(n * batch, DT[suf], seed=logn * 5 + P + j)
     if j:

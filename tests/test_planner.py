@@ -18,10 +18,11 @@ def test_config1_2e20_fp64_one_worker():
 def test_config2_2e20_fp64_eight_workers_one_gpu(monkeypatch):
     d = pifft.dry_run(1 << 20, 8, 1, F64)
     # the worker-interleaved layout with every worker's tree fused into the
-    # first pass (MODE 11: 8 adjacent line indices x 8 workers, first radix
-    # 128), the last pass storing natural order itself: two launches
+    # first pass (MODE 11: 4 adjacent line indices x 8 workers at the 4096-value
+    # tile -- 256 workgroups --, first radix 128), the last pass storing
+    # natural order itself: two launches
     assert d["worker_interleaved"] and d["launch_kind"] == ["tree+pass", "pass"]
-    assert d["launch_mode"] == [11, 10] and d["radix"] == [128, 1024] and d["lines"] == [64, 8]
+    assert d["launch_mode"] == [11, 10] and d["radix"] == [128, 1024] and d["lines"] == [32, 8]
     assert d["local_n"] == 1 << 17 and d["out_elems"] == 1 << 20
     assert d["launch_bytes"] == [2 * (1 << 20) * 16] * 2  # each leaf read once, every value written once
     monkeypatch.setenv("PIFFT_WIL_FUSE", "0")  # the tree as its own launch
@@ -30,19 +31,38 @@ def test_config2_2e20_fp64_eight_workers_one_gpu(monkeypatch):
 
 def test_fused_all_worker_rule():
     """Which all-worker plans fuse the tree into the first pass (MODE 11) and
-    at which J (the tile's adjacent line indices: first radix 8192 / (J P)) --
-    the planner's measured rule (profiles/r05m_wil_fuse_j.log)."""
+    at which J (the tile's adjacent line indices: first radix tile / (J P)) --
+    the planner's measured rule (profiles/r05m_wil_fuse_j.log; the 4096-value
+    tile and J = 4 refinements: r05s-u_*)."""
     def first(n, P, prec, b=1):
         d = pifft.dry_run(n, P, b, prec)
         return d["launch_mode"][0], d["radix"][0], d["lines"][0]
-    assert first(1 << 20, 8, F64) == (11, 128, 64)     # fp64 P <= 8: J = 8
+    assert first(1 << 21, 8, F64) == (11, 128, 64)     # fp64 P <= 8: J = 8
     assert first(1 << 28, 8, F64) == (11, 128, 64)
-    assert first(1 << 20, 2, F64) == (11, 512, 16)
+    assert first(1 << 21, 2, F64) == (11, 512, 16)
     assert first(1 << 22, 16, F64)[0] == 0               # fp64 P = 16 below 256 MiB: the tree launch
     assert first(1 << 28, 16, F64) == (11, 64, 128)     # ... and from 256 MiB fused
-    assert first(1 << 20, 8, F32) == (11, 128, 64)      # fp32 up to 32 MiB: J = 8
+    assert first(1 << 21, 2, F32) == (11, 512, 16)      # fp32 up to 32 MiB: J = 8
     assert first(1 << 24, 8, F32) == (11, 64, 128)      # up to 1 GiB: J = 16
     assert first(1 << 28, 8, F32)[0] == 0                # beyond: the tree launch
+    # fewer than 256 workgroups at the 8192-value tile (<= 2^20 values): the
+    # 4096-value tile at J = 4, both precisions, batch counted
+    assert first(1 << 20, 8, F64) == (11, 128, 32)
+    assert first(1 << 20, 2, F64) == (11, 512, 8)
+    assert first(1 << 18, 4, F64, b=4) == (11, 256, 16)
+    assert first(1 << 19, 4, F64, b=4) == (11, 256, 32)  # 2^21 values: the 8192 tile, J = 8
+    assert first(1 << 20, 8, F32) == (11, 128, 32)
+    # J = 8 would leave a remainder split in two passes, J = 4 one: J = 4 (fp64
+    # P <= 8; fp32 only at P = 8, from a 2048-point remainder)
+    for P in (2, 4, 8):
+        d = pifft.dry_run(1 << 22, P, 1, F64)
+        assert d["launch_mode"] == [11, 10] and d["lines"][0] == 4 * P and d["radix"][1] == 2048
+    assert pifft.dry_run(1 << 21, 8, 1, F64)["radix"] == [128, 2048]   # a 2048-point remainder: J = 8
+    assert pifft.dry_run(1 << 23, 8, 1, F64)["radix"] == [128, 128, 64]  # J = 4 splits too: J = 8
+    assert pifft.dry_run(1 << 21, 8, 1, F32)["radix"] == [256, 1024]
+    assert pifft.dry_run(1 << 22, 8, 1, F32)["radix"] == [256, 2048]
+    assert pifft.dry_run(1 << 22, 4, 1, F32)["radix"] == [256, 64, 64]  # fp32 P = 4 keeps J = 8
+    assert pifft.dry_run(1 << 22, 16, 1, F32)["lines"][0] == 128        # ... and P = 16
 
 
 def test_natural_store_rule(monkeypatch):

@@ -119,6 +119,15 @@ for T, prec, js in (("double", 64, (16, 8, 4)), ("float", 32, (32, 16, 8))):
                 continue
             for nts in (0, 1):
                 items.append(f"PK({T}, {prec}, {R}, {C}, 11, {nts}, {lp}),")
+# ... and the planner's two refinements for P <= 8 (profiles/r05s-u_*): the
+# 4096-value tile at J = 4 for grids of fewer than 256 workgroups (both
+# precisions), and fp32 J = 4 at P = 8 (a 2048-point remainder or longer)
+for T, prec in (("double", 64), ("float", 32)):
+    for lp in (1, 2, 3):
+        for nts in (0, 1):
+            items.append(f"PK({T}, {prec}, {4096 // (4 << lp)}, {4 << lp}, 11, {nts}, {lp}),")
+for nts in (0, 1):
+    items.append(f"PK(float, 32, 256, 32, 11, {nts}, 3),")
 # (config 2's slice with its fused tree pass at C = 2 -- 128 workgroups
 # gathering leaves, 32-B leaf segments: +0.7 % on the slice, 0 to +2.4 % on
 # neighbouring slices, within run-to-run noise; round 4,

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--variants", default="[{}]")
     ap.add_argument("--flags", type=int, default=-1, help="plan flags (default: natural / slices)")
+    ap.add_argument("--check", action="store_true",
+                    help="each variant's output against the first variant's (relative L2)")
     ap.add_argument("--tune-ws", type=int, default=0,
                     help="workspace placements tried per plan (pifft_plan_tune_workspace, as bench.py does)")
     args = ap.parse_args()
@@ -40,6 +42,7 @@ def main():
     x = torch.empty(n * args.batch, dtype=cdt, device="cuda")
     pifft.generate_device(x.data_ptr(), n * args.batch, n, prec)
     y = None
+    yref = None
     # reference ceiling: torch's device copy of the same bytes
     z = torch.empty_like(x)
     for _ in range(3):
@@ -100,8 +103,15 @@ def main():
         per = " | ".join(f"{k}{'x' + str(c) if c > 1 else ''} {ms:.3f}ms {b / ms / 1e6:.0f}GB/s"
                          for k, ms, b, c in groups)
         gf = 5.0 * n * args.log_n * args.batch / (wall * 1e-3) / 1e9
-        print(f"{json.dumps(var)} radix={d['radix']} lines={d['lines']} wall {wall:.3f} ms {gf:.0f} GFLOP/s "
-              f"(sum of launches {tot:.3f} ms) :: {per}", flush=True)
+        chk = ""
+        if args.check:
+            if yref is None:
+                yref = y.clone()
+            else:
+                rel = ((y - yref).abs().pow(2).sum() / yref.abs().pow(2).sum()).sqrt().item()
+                chk = f" [vs first variant: rel L2 {rel:.2e}]"
+        print(f"{json.dumps(var)} radix={d['radix']} lines={d['lines']} vpt={d.get('vpt')} wall {wall:.3f} ms "
+              f"{gf:.0f} GFLOP/s (sum of launches {tot:.3f} ms) :: {per}{chk}", flush=True)
         del plan
 
 
