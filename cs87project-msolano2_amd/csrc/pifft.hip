@@ -415,17 +415,17 @@ bool use_vpt32(int prec, uint64_t M, uint64_t ntrans, int heavy_lp) {
 // pos_ok: the position-aware pass rates may price this plan (not for the
 // worker-interleaved layout, whose passes move rows of all workers: there the
 // narrow pass last measured 1-14 % slower, profiles/r03_pos_model_shapes.log)
+// single_max: the longest one-pass local FFT (log2; default 14, PIFFT_SINGLE_MAX_LOG)
 int plan_passes(uint64_t M, int prec, uint64_t ntrans, std::vector<PassChoice>& out, int heavy_lp = 0,
-                bool allow_v32 = true, bool pos_ok = true) {
+                bool allow_v32 = true, bool pos_ok = true, int single_max = -1) {
     out.clear();
     if (M <= 1) return 0;
     const int logm = ilog2u(M);
     const size_t esz = prec == 64 ? 16 : 8;
-    const bool v32 = allow_v32 && M > (1ull << env_int("PIFFT_SINGLE_MAX_LOG", 14)) &&
-                     use_vpt32(prec, M, ntrans, heavy_lp);
+    if (single_max < 0) single_max = env_int("PIFFT_SINGLE_MAX_LOG", 14);
+    const bool v32 = allow_v32 && M > (1ull << single_max) && use_vpt32(prec, M, ntrans, heavy_lp);
     const int stile = v32 ? 16384 : 0;
     const int nts = pick_nts(2 * ntrans * M * esz);
-    const int single_max = env_int("PIFFT_SINGLE_MAX_LOG", 14);
     if (logm <= single_max) {
         const int R = (int)M;
         const int C = pick_lines(prec, R, ntrans, ntrans, prec == 64 ? "PIFFT_SINGLE_C64" : "PIFFT_SINGLE_C32", 0);
@@ -658,6 +658,17 @@ int build_plan(pifft_plan* p, bool dry = false) {
             p->wil = true;
         }
     }
+    // A single transform whose local FFT is one pass (M <= 2^14) would run
+    // tree + pass + interleave launches.  From M = 2^12 up the
+    // worker-interleaved plan with every worker's tree fused into its first
+    // pass (MODE 11 below: the first radix, then an M / R1-point pass) does
+    // it in two, kept only where that fused plan exists (round 5,
+    // profiles/r05w_small_wil.log: fp64 2^15 P = 2 22 -> 13 us, 2^16 P = 4
+    // 23 -> 11, 2^17 P = 8 25 -> 12; fp32 2^17 P = 8 21 -> 9, 2^18 P = 16
+    // 25 -> 13; 9-30 % at the other sizes).  PIFFT_WIL_SINGLE=0: off.
+    const bool wil_single = wil_ok && passes.size() == 1 && p->batch == 1 && p->m >= 4096 &&
+                            env_int("PIFFT_WIL_SINGLE", 1);
+    if (wil_single) p->wil = true;
     // The worker-interleaved plan with its tree fused into the first pass
     // (MODE 11, k_pass wil_tree_to_lds): a tile of J adjacent line indices x
     // all P workers loads each position's P leaves once (J esz-byte leaf
@@ -733,6 +744,16 @@ int build_plan(pifft_plan* p, bool dry = false) {
             for (const auto& pc : rest) passes.push_back(pc);
             wil_fused_c = (uint32_t)C1;
         }
+    }
+    if (wil_single && !wil_fused_c) {
+        // no fused plan: the single pass -- except P = 16 at fp64 (no fused
+        // pass below 256 MiB, above), where the worker-interleaved two-pass
+        // plan after its tree launch still saves the interleave launch (2^16
+        // 16 -> 15 us, 2^17 21 -> 16, 2^18 30 -> 19; r05w_small_wil.log)
+        std::vector<PassChoice> w;
+        p->wil = p->lp == 4 && plan_passes(p->m, p->prec, ntrans, w, 0, false, false, ilog2u(p->m) - 1) == 0 &&
+                 w.size() == 2 && to_wil(w);
+        if (p->wil) passes = w;
     }
     if (p->bitrev && !passes.empty()) {
         // the last pass stores in bit-reversed order: its MODE | 4 twin, at

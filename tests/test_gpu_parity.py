@@ -812,7 +812,9 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
                                                 ("f64", 24, 8, 1, 0), ("f32", 23, 4, 1, 0), ("f64", 19, 16, 1, 8),
                                                 ("f32", 20, 8, 1, 16), ("f64", 20, 2, 1, 0), ("f64", 22, 4, 1, 0),
                                                 ("f64", 22, 8, 1, 0), ("f32", 21, 8, 1, 0), ("f32", 22, 8, 1, 0),
-                                                ("f64", 17, 4, 1, 0), ("f32", 18, 8, 2, 0)])
+                                                ("f64", 17, 4, 1, 0), ("f32", 18, 8, 2, 0), ("f64", 17, 8, 1, 0),
+                                                ("f64", 14, 2, 1, 0), ("f64", 15, 4, 1, 0), ("f32", 16, 16, 1, 0),
+                                                ("f32", 16, 8, 1, 0)])
 def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
     """All-worker natural-order plans with every worker's tree fused into the
     first worker-interleaved pass (MODE 11: each position's P leaves loaded
@@ -836,6 +838,28 @@ def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
     sep = pifft.Plan(n, P, batch, PREC[suf])
     assert sep.describe()["launch_kind"][0] == "tree"
     assert rel_l2(run(sep, x), got.reshape(-1)) <= tol(suf, n)
+
+
+@pytest.mark.parametrize("suf,logn,P", [("f64", 17, 16), ("f64", 18, 16), ("f64", 16, 16), ("f64", 15, 4),
+                                       ("f64", 12, 2), ("f32", 17, 8), ("f32", 14, 2), ("f64", 14, 8)])
+def test_single_pass_all_worker_plans_two_pass(suf, logn, P, monkeypatch):
+    """A single transform whose local FFT is one pass (N / P <= 2^14) runs the
+    two-pass worker-interleaved plan from 2^12 points up (the fused tree pass,
+    or at fp64 P = 16 the tree launch and two passes): against the oracle and
+    against the single-pass plan (PIFFT_WIL_SINGLE=0), within tolerance (the
+    radices differ).  Below 2^12 points the single pass stays."""
+    n = 1 << logn
+    x = oracle.generate(n, DT[suf], seed=logn * 7 + P)
+    plan = pifft.Plan(n, P, 1, PREC[suf])
+    d = plan.describe()
+    two = (n // P) >= 4096
+    assert d["worker_interleaved"] == two and ("interleave" in d["launch_kind"]) != two, d
+    got = run(plan, x)
+    assert_bins_close(got, oracle.fft(x, P=1, nthreads=8), suf, n)
+    monkeypatch.setenv("PIFFT_WIL_SINGLE", "0")
+    single = pifft.Plan(n, P, 1, PREC[suf])
+    assert single.describe()["launch_kind"] == ["tree", "pass", "interleave"]
+    assert rel_l2(run(single, x), got) <= tol(suf, n)
 
 
 # ------------------------------------------------ the final exchange (8e) ---

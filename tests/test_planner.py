@@ -65,6 +65,28 @@ def test_fused_all_worker_rule():
     assert pifft.dry_run(1 << 22, 16, 1, F32)["lines"][0] == 128        # ... and P = 16
 
 
+def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
+    """A single transform whose local FFT would be one pass (M <= 2^14) runs
+    the worker-interleaved plan with every worker's tree fused into its first
+    pass -- two launches instead of tree + pass + interleave -- from M = 2^12
+    up where that plan exists; fp64 P = 16 (no fused pass there) the
+    worker-interleaved two-pass plan after its tree launch (profiles/
+    r05w_small_wil.log).  Batched plans and M < 2^12 keep the single pass."""
+    def kinds(n, P, prec, b=1):
+        return pifft.dry_run(n, P, b, prec)["launch_kind"]
+    assert kinds(1 << 17, 8, F64) == ["tree+pass", "pass"]
+    assert pifft.dry_run(1 << 17, 8, 1, F64)["radix"] == [128, 128]
+    assert kinds(1 << 14, 2, F64) == ["tree+pass", "pass"]
+    assert kinds(1 << 16, 16, F32) == ["tree+pass", "pass"]
+    assert kinds(1 << 18, 16, F64) == ["tree", "pass", "pass"]
+    assert pifft.dry_run(1 << 18, 16, 1, F64)["worker_interleaved"]
+    assert kinds(1 << 14, 8, F64) == ["tree", "pass", "interleave"]     # M = 2^11
+    assert kinds(1 << 15, 16, F64) == ["tree", "pass", "interleave"]
+    assert kinds(1 << 15, 4, F64, b=4) == ["tree", "pass", "interleave"]  # batched
+    monkeypatch.setenv("PIFFT_WIL_SINGLE", "0")
+    assert kinds(1 << 17, 8, F64) == ["tree", "pass", "interleave"]
+
+
 def test_natural_store_rule(monkeypatch):
     """The planner's rule for the last pass storing natural order itself
     (pifft.hip build_plan, PIFFT_ILV) on the slice-major layout (multi-pass
@@ -229,13 +251,14 @@ def test_worker_interleaved_layout(monkeypatch):
     """All P <= 16 workers of a natural-order plan with a multi-pass local FFT
     use the worker-interleaved layout: tree + passes, no interleave launch and
     no scattered natural-order store; PIFFT_WORKER_IL=0 restores the
-    slice-major layout.  Single-pass local FFTs, P > 16 and worker ranges keep
+    slice-major layout.  Single-pass local FFTs below 2^12 points (from 2^12
+    the plan goes two-pass worker-interleaved), P > 16 and worker ranges keep
     the slice-major layout."""
     d = pifft.dry_run(1 << 20, 8, 1, F64)
     assert d["worker_interleaved"] and not d["natural_store"] and d["launch_kind"] == ["tree+pass", "pass"]
     big = pifft.dry_run(1 << 28, 8, 1, F64)
     assert big["worker_interleaved"] and "interleave" not in big["launch_kind"]
-    assert not pifft.dry_run(1 << 16, 8, 1, F64)["worker_interleaved"]          # single-pass local FFT
+    assert not pifft.dry_run(1 << 14, 8, 1, F64)["worker_interleaved"]          # single-pass local FFT
     assert not pifft.dry_run(1 << 20, 32, 1, F64)["worker_interleaved"]         # two tree launches
     assert not pifft.dry_run(1 << 20, 8, 1, F64, first=0, count=4)["worker_interleaved"]
     assert not pifft.dry_run(1 << 20, 1, 1, F64)["worker_interleaved"]
@@ -277,7 +300,8 @@ STRAY = {"PIFFT_ORDER": "1", "PIFFT_PASSES": "4", "PIFFT_RADIX_LOGS": "10,10,8",
          "PIFFT_TILE64": "4096", "PIFFT_LAST_C": "16", "PIFFT_FUSE_TREE": "0", "PIFFT_ILV": "1",
          "PIFFT_SINGLE_TILE32": "8192", "PIFFT_LAST_VPT": "16", "PIFFT_FUSED_VPT": "16", "PIFFT_WIL_VPT": "16",
          "PIFFT_WIL_FUSE": "0", "PIFFT_WIL_FUSE_J": "16", "PIFFT_WIL_TREE_DIRECT": "1", "PIFFT_WIL_TREE_MIN_LOG": "0",
-         "PIFFT_PERMLANE": "0", "PIFFT_FAULT": "broadcast"}
+         "PIFFT_PERMLANE": "0", "PIFFT_FAULT": "broadcast",
+         "PIFFT_WIL_FUSE_TILE": "2048", "PIFFT_WIL_SINGLE": "0"}
 
 
 @pytest.mark.parametrize("shape", [(1 << 28, 1, 1, F64, 0, 1, 0), (1 << 28, 1, 1, F32, 0, 1, 0),
