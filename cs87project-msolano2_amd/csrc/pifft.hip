@@ -666,8 +666,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // profiles/r05w_small_wil.log: fp64 2^15 P = 2 22 -> 13 us, 2^16 P = 4
     // 23 -> 11, 2^17 P = 8 25 -> 12; fp32 2^17 P = 8 21 -> 9, 2^18 P = 16
     // 25 -> 13; 9-30 % at the other sizes).  PIFFT_WIL_SINGLE=0: off.
-    const bool wil_single = wil_ok && passes.size() == 1 && p->batch == 1 && p->m >= 4096 &&
-                            env_int("PIFFT_WIL_SINGLE", 1);
+    // And a transform that fits one tile (P M <= 8192 values, from 1024: the
+    // reference's own GPU sweep, cuda/run-experiments:16) runs every worker's
+    // tree and its whole M-point FFT in ONE launch: the fused pass at J = 1 (C
+    // = P lines of R = M points) storing natural order (PIFFT_WIL_ONE_LAUNCH=0:
+    // off).
+    const uint64_t pm = (uint64_t)p->P * p->m;
+    const bool wil_single = wil_ok && passes.size() == 1 && p->batch == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
+                            (p->m >= 4096 || (pm <= 8192 && pm >= 1024 && env_int("PIFFT_WIL_ONE_LAUNCH", 1)));
     if (wil_single) p->wil = true;
     // The worker-interleaved plan with its tree fused into the first pass
     // (MODE 11, k_pass wil_tree_to_lds): a tile of J adjacent line indices x
@@ -704,7 +710,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // PIFFT_WIL_FUSE_TILE says otherwise), PIFFT_WIL_FUSE_TILE: the tile
     // (values), PIFFT_WIL_FUSE_VPT: values per thread (tuning, tests).
     uint32_t wil_fused_c = 0;
-    if (p->wil && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
+    if (wil_single && p->m < 4096 && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
+        const int nts0 = pick_nts(2 * ntrans * p->m * esz);
+        if (find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp)) {
+            passes = {PassChoice{(int)p->m, (int)p->P, 11, nts0}};
+            wil_fused_c = p->P;
+        }
+    }
+    if (p->wil && !wil_fused_c && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
         const uint64_t data = (uint64_t)p->batch * p->n * esz;
         const int jdef = p->prec == 64 ? ((p->lp <= 3 || data >= (256ull << 20)) ? 8 : 0)
                                        : (data <= (32ull << 20) ? 8 : data <= (1ull << 30) ? 16 : 0);
@@ -751,7 +764,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         // plan after its tree launch still saves the interleave launch (2^16
         // 16 -> 15 us, 2^17 21 -> 16, 2^18 30 -> 19; r05w_small_wil.log)
         std::vector<PassChoice> w;
-        p->wil = p->lp == 4 && plan_passes(p->m, p->prec, ntrans, w, 0, false, false, ilog2u(p->m) - 1) == 0 &&
+        p->wil = p->lp == 4 && p->m >= 4096 && plan_passes(p->m, p->prec, ntrans, w, 0, false, false, ilog2u(p->m) - 1) == 0 &&
                  w.size() == 2 && to_wil(w);
         if (p->wil) passes = w;
     }

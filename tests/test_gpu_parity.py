@@ -840,26 +840,54 @@ def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
     assert rel_l2(run(sep, x), got.reshape(-1)) <= tol(suf, n)
 
 
-@pytest.mark.parametrize("suf,logn,P", [("f64", 17, 16), ("f64", 18, 16), ("f64", 16, 16), ("f64", 15, 4),
-                                       ("f64", 12, 2), ("f32", 17, 8), ("f32", 14, 2), ("f64", 14, 8)])
-def test_single_pass_all_worker_plans_two_pass(suf, logn, P, monkeypatch):
+ONE = ["tree+pass"]
+TWO = ["tree+pass", "pass"]
+THREE = ["tree", "pass", "interleave"]
+
+
+@pytest.mark.parametrize("suf,logn,P,kinds", [("f64", 17, 16, ["tree", "pass", "pass"]), ("f64", 18, 16, ["tree", "pass", "pass"]),
+                                             ("f64", 16, 16, ["tree", "pass", "pass"]), ("f64", 15, 4, TWO),
+                                             ("f32", 17, 8, TWO), ("f32", 14, 2, TWO), ("f64", 14, 8, THREE),
+                                             ("f64", 13, 2, THREE), ("f64", 12, 2, ONE)])
+def test_single_pass_all_worker_plans_two_pass(suf, logn, P, kinds, monkeypatch):
     """A single transform whose local FFT is one pass (N / P <= 2^14) runs the
-    two-pass worker-interleaved plan from 2^12 points up (the fused tree pass,
-    or at fp64 P = 16 the tree launch and two passes): against the oracle and
-    against the single-pass plan (PIFFT_WIL_SINGLE=0), within tolerance (the
-    radices differ).  Below 2^12 points the single pass stays."""
+    two-pass worker-interleaved plan from 2^12 points per worker up (the fused
+    tree pass, or at fp64 P = 16 the tree launch and two passes), and a
+    transform of P M <= 8192 values (M < 4096) one fused launch: against the
+    oracle and against the three-launch plan (PIFFT_WIL_SINGLE=0), within
+    tolerance (the radices differ)."""
     n = 1 << logn
     x = oracle.generate(n, DT[suf], seed=logn * 7 + P)
     plan = pifft.Plan(n, P, 1, PREC[suf])
     d = plan.describe()
-    two = (n // P) >= 4096
-    assert d["worker_interleaved"] == two and ("interleave" in d["launch_kind"]) != two, d
+    assert d["launch_kind"] == kinds and d["worker_interleaved"] == (kinds != THREE), d
     got = run(plan, x)
     assert_bins_close(got, oracle.fft(x, P=1, nthreads=8), suf, n)
     monkeypatch.setenv("PIFFT_WIL_SINGLE", "0")
     single = pifft.Plan(n, P, 1, PREC[suf])
-    assert single.describe()["launch_kind"] == ["tree", "pass", "interleave"]
+    assert single.describe()["launch_kind"] == THREE
     assert rel_l2(run(single, x), got) <= tol(suf, n)
+
+
+@pytest.mark.parametrize("suf", ["f64", "f32"])
+@pytest.mark.parametrize("logn", [10, 11, 12, 13])
+@pytest.mark.parametrize("P", [2, 4, 8, 16])
+def test_tiny_all_worker_plans_one_launch(suf, logn, P, monkeypatch):
+    """The reference's own GPU sweep grid (cuda/run-experiments:16-17: n =
+    1024-8192, p up to 16 here): one fused launch -- every worker's tree,
+    then its whole N/P-point FFT, natural-order store -- where N/P < 4096,
+    against the oracle and the three-launch plan."""
+    n = 1 << logn
+    x = oracle.generate(n, DT[suf], seed=logn * 3 + P)
+    plan = pifft.Plan(n, P, 1, PREC[suf])
+    kinds = plan.describe()["launch_kind"]
+    assert kinds == (ONE if n // P < 4096 else THREE), kinds
+    got = run(plan, x)
+    assert_bins_close(got, oracle.fft(x, P=1, nthreads=8), suf, n)
+    monkeypatch.setenv("PIFFT_WIL_ONE_LAUNCH", "0")
+    three = pifft.Plan(n, P, 1, PREC[suf])
+    assert three.describe()["launch_kind"] == THREE
+    assert rel_l2(run(three, x), got) <= tol(suf, n)
 
 
 # ------------------------------------------------ the final exchange (8e) ---

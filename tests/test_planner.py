@@ -87,6 +87,24 @@ def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
     assert kinds(1 << 17, 8, F64) == ["tree", "pass", "interleave"]
 
 
+def test_tiny_all_worker_plans_one_launch(monkeypatch):
+    """A single transform of P M <= 8192 values (from 1024, M < 4096: the
+    reference's GPU sweep sizes) runs as ONE fused pass: J = 1, C = P lines
+    of R = M points, every worker's tree then its whole local FFT, storing
+    natural order."""
+    for prec in (F64, F32):
+        for n, P in ((1 << 10, 2), (1 << 10, 16), (1 << 12, 8), (1 << 13, 4), (1 << 13, 16)):
+            d = pifft.dry_run(n, P, 1, prec)
+            assert d["launch_kind"] == ["tree+pass"] and d["launch_mode"] == [11], (n, P, d)
+            assert d["radix"] == [n // P] and d["lines"] == [P] and d["worker_interleaved"]
+    assert pifft.dry_run(1 << 13, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]  # M = 4096
+    assert pifft.dry_run(1 << 13, 32, 1, F64)["launch_kind"][-1] == "interleave"               # P = 32
+    assert pifft.dry_run(1 << 9, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]   # < 1024
+    assert pifft.dry_run(1 << 12, 8, 2, F64)["launch_kind"][0] == "tree"                       # batched
+    monkeypatch.setenv("PIFFT_WIL_ONE_LAUNCH", "0")
+    assert pifft.dry_run(1 << 12, 8, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]
+
+
 def test_natural_store_rule(monkeypatch):
     """The planner's rule for the last pass storing natural order itself
     (pifft.hip build_plan, PIFFT_ILV) on the slice-major layout (multi-pass
@@ -301,7 +319,7 @@ STRAY = {"PIFFT_ORDER": "1", "PIFFT_PASSES": "4", "PIFFT_RADIX_LOGS": "10,10,8",
          "PIFFT_SINGLE_TILE32": "8192", "PIFFT_LAST_VPT": "16", "PIFFT_FUSED_VPT": "16", "PIFFT_WIL_VPT": "16",
          "PIFFT_WIL_FUSE": "0", "PIFFT_WIL_FUSE_J": "16", "PIFFT_WIL_TREE_DIRECT": "1", "PIFFT_WIL_TREE_MIN_LOG": "0",
          "PIFFT_PERMLANE": "0", "PIFFT_FAULT": "broadcast",
-         "PIFFT_WIL_FUSE_TILE": "2048", "PIFFT_WIL_SINGLE": "0"}
+         "PIFFT_WIL_FUSE_TILE": "2048", "PIFFT_WIL_SINGLE": "0", "PIFFT_WIL_ONE_LAUNCH": "0"}
 
 
 @pytest.mark.parametrize("shape", [(1 << 28, 1, 1, F64, 0, 1, 0), (1 << 28, 1, 1, F32, 0, 1, 0),

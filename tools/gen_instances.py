@@ -128,6 +128,14 @@ for T, prec in (("double", 64), ("float", 32)):
             items.append(f"PK({T}, {prec}, {4096 // (4 << lp)}, {4 << lp}, 11, {nts}, {lp}),")
 for nts in (0, 1):
     items.append(f"PK(float, 32, 256, 32, 11, {nts}, 3),")
+# ... and the one-launch form: a transform of P M <= 8192 values (from 1024)
+# as ONE fused pass at J = 1 -- C = P lines of R = M points, every worker's
+# tree then its whole M-point FFT, natural-order store (round 5; the
+# reference's GPU sweep sizes, n = 1024-8192, p <= 16)
+for T, prec in (("double", 64), ("float", 32)):
+    for lp in (1, 2, 3, 4):
+        for logm in range(10 - lp, min(14 - lp, 12)):  # (M < 4096: fp64 P = 2 at 4096 spills)
+            items.append(f"PK({T}, {prec}, {1 << logm}, {1 << lp}, 11, 0, {lp}),")
 # (config 2's slice with its fused tree pass at C = 2 -- 128 workgroups
 # gathering leaves, 32-B leaf segments: +0.7 % on the slice, 0 to +2.4 % on
 # neighbouring slices, within run-to-run noise; round 4,
