@@ -659,7 +659,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         }
     }
     // A single transform whose local FFT is one pass (M <= 2^14) would run
-    // tree + pass + interleave launches.  From M = 2^12 up the
+    // tree + pass + interleave launches.  From M = 2^11 up the
     // worker-interleaved plan with every worker's tree fused into its first
     // pass (MODE 11 below: the first radix, then an M / R1-point pass) does
     // it in two, kept only where that fused plan exists (round 5,
@@ -671,9 +671,18 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // tree and its whole M-point FFT in ONE launch: the fused pass at J = 1 (C
     // = P lines of R = M points) storing natural order (PIFFT_WIL_ONE_LAUNCH=0:
     // off).
+    // The two-pass plan from M = 2^11 (fp64 2^14 P = 8 11 -> 10 us, fp32 8 vs
+    // 11, fp32 2^15 P = 16 12 vs 14: profiles/r05za_small_plan_edges.log).
+    // (PIFFT_WIL_ONE_MAX: the largest one-launch transform, values -- 16384
+    // measured slower; the instances exist only where they compile spill-free.
+    // PIFFT_WIL_SINGLE_MIN_LOG: the two-pass plan's smallest M, log2.  Tuning.)
     const uint64_t pm = (uint64_t)p->P * p->m;
+    const int nts0 = pick_nts(2 * ntrans * p->m * esz);
+    const bool one_ok = wil_ok && passes.size() == 1 && pm >= 1024 &&
+                        pm <= (uint64_t)env_int("PIFFT_WIL_ONE_MAX", 8192) && env_int("PIFFT_WIL_ONE_LAUNCH", 1) &&
+                        find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp);
     const bool wil_single = wil_ok && passes.size() == 1 && p->batch == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
-                            (p->m >= 4096 || (pm <= 8192 && pm >= 1024 && env_int("PIFFT_WIL_ONE_LAUNCH", 1)));
+                            (p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11)) || one_ok);
     if (wil_single) p->wil = true;
     // The worker-interleaved plan with its tree fused into the first pass
     // (MODE 11, k_pass wil_tree_to_lds): a tile of J adjacent line indices x
@@ -710,12 +719,9 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // PIFFT_WIL_FUSE_TILE says otherwise), PIFFT_WIL_FUSE_TILE: the tile
     // (values), PIFFT_WIL_FUSE_VPT: values per thread (tuning, tests).
     uint32_t wil_fused_c = 0;
-    if (wil_single && p->m < 4096 && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
-        const int nts0 = pick_nts(2 * ntrans * p->m * esz);
-        if (find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp)) {
-            passes = {PassChoice{(int)p->m, (int)p->P, 11, nts0}};
-            wil_fused_c = p->P;
-        }
+    if (wil_single && one_ok && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
+        passes = {PassChoice{(int)p->m, (int)p->P, 11, nts0}};
+        wil_fused_c = p->P;
     }
     if (p->wil && !wil_fused_c && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
         const uint64_t data = (uint64_t)p->batch * p->n * esz;

@@ -847,11 +847,12 @@ THREE = ["tree", "pass", "interleave"]
 
 @pytest.mark.parametrize("suf,logn,P,kinds", [("f64", 17, 16, ["tree", "pass", "pass"]), ("f64", 18, 16, ["tree", "pass", "pass"]),
                                              ("f64", 16, 16, ["tree", "pass", "pass"]), ("f64", 15, 4, TWO),
-                                             ("f32", 17, 8, TWO), ("f32", 14, 2, TWO), ("f64", 14, 8, THREE),
+                                             ("f32", 17, 8, TWO), ("f32", 14, 2, TWO), ("f64", 14, 8, TWO),
+                                             ("f64", 14, 16, THREE), ("f32", 15, 16, TWO),
                                              ("f64", 13, 2, THREE), ("f64", 12, 2, ONE)])
 def test_single_pass_all_worker_plans_two_pass(suf, logn, P, kinds, monkeypatch):
     """A single transform whose local FFT is one pass (N / P <= 2^14) runs the
-    two-pass worker-interleaved plan from 2^12 points per worker up (the fused
+    two-pass worker-interleaved plan from 2^11 points per worker up (the fused
     tree pass, or at fp64 P = 16 the tree launch and two passes), and a
     transform of P M <= 8192 values (M < 4096) one fused launch: against the
     oracle and against the three-launch plan (PIFFT_WIL_SINGLE=0), within
@@ -881,7 +882,7 @@ def test_tiny_all_worker_plans_one_launch(suf, logn, P, monkeypatch):
     x = oracle.generate(n, DT[suf], seed=logn * 3 + P)
     plan = pifft.Plan(n, P, 1, PREC[suf])
     kinds = plan.describe()["launch_kind"]
-    assert kinds == (ONE if n // P < 4096 else THREE), kinds
+    assert kinds == (ONE if n // P < 4096 or (suf == "f32" and P == 2) else THREE), kinds
     got = run(plan, x)
     assert_bins_close(got, oracle.fft(x, P=1, nthreads=8), suf, n)
     monkeypatch.setenv("PIFFT_WIL_ONE_LAUNCH", "0")

@@ -69,7 +69,7 @@ def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
     """A single transform whose local FFT would be one pass (M <= 2^14) runs
     the worker-interleaved plan with every worker's tree fused into its first
     pass -- two launches instead of tree + pass + interleave -- from M = 2^12
-    up where that plan exists; fp64 P = 16 (no fused pass there) the
+    up (2^11 at the fused plans) where that plan exists; fp64 P = 16 (no fused pass there) the
     worker-interleaved two-pass plan after its tree launch (profiles/
     r05w_small_wil.log).  Batched plans and M < 2^12 keep the single pass."""
     def kinds(n, P, prec, b=1):
@@ -80,7 +80,8 @@ def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
     assert kinds(1 << 16, 16, F32) == ["tree+pass", "pass"]
     assert kinds(1 << 18, 16, F64) == ["tree", "pass", "pass"]
     assert pifft.dry_run(1 << 18, 16, 1, F64)["worker_interleaved"]
-    assert kinds(1 << 14, 8, F64) == ["tree", "pass", "interleave"]     # M = 2^11
+    assert kinds(1 << 14, 8, F64) == ["tree+pass", "pass"]               # M = 2^11
+    assert kinds(1 << 14, 16, F64) == ["tree", "pass", "interleave"]    # M = 2^10
     assert kinds(1 << 15, 16, F64) == ["tree", "pass", "interleave"]
     assert kinds(1 << 15, 4, F64, b=4) == ["tree", "pass", "interleave"]  # batched
     monkeypatch.setenv("PIFFT_WIL_SINGLE", "0")
@@ -88,7 +89,7 @@ def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
 
 
 def test_tiny_all_worker_plans_one_launch(monkeypatch):
-    """A single transform of P M <= 8192 values (from 1024, M < 4096: the
+    """A single transform of P M <= 8192 values (from 1024, M < 4096 but fp32 P = 2: the
     reference's GPU sweep sizes) runs as ONE fused pass: J = 1, C = P lines
     of R = M points, every worker's tree then its whole local FFT, storing
     natural order."""
@@ -98,6 +99,7 @@ def test_tiny_all_worker_plans_one_launch(monkeypatch):
             assert d["launch_kind"] == ["tree+pass"] and d["launch_mode"] == [11], (n, P, d)
             assert d["radix"] == [n // P] and d["lines"] == [P] and d["worker_interleaved"]
     assert pifft.dry_run(1 << 13, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]  # M = 4096
+    assert pifft.dry_run(1 << 13, 2, 1, F32)["launch_kind"] == ["tree+pass"]                    # (spill-free)
     assert pifft.dry_run(1 << 13, 32, 1, F64)["launch_kind"][-1] == "interleave"               # P = 32
     assert pifft.dry_run(1 << 9, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]   # < 1024
     assert pifft.dry_run(1 << 12, 8, 2, F64)["launch_kind"][0] == "tree"                       # batched
@@ -269,14 +271,14 @@ def test_worker_interleaved_layout(monkeypatch):
     """All P <= 16 workers of a natural-order plan with a multi-pass local FFT
     use the worker-interleaved layout: tree + passes, no interleave launch and
     no scattered natural-order store; PIFFT_WORKER_IL=0 restores the
-    slice-major layout.  Single-pass local FFTs below 2^12 points (from 2^12
-    the plan goes two-pass worker-interleaved), P > 16 and worker ranges keep
+    slice-major layout.  Single-pass local FFTs that neither fit one fused
+    launch nor reach 2^11 points (from there two-pass worker-interleaved), P > 16 and worker ranges keep
     the slice-major layout."""
     d = pifft.dry_run(1 << 20, 8, 1, F64)
     assert d["worker_interleaved"] and not d["natural_store"] and d["launch_kind"] == ["tree+pass", "pass"]
     big = pifft.dry_run(1 << 28, 8, 1, F64)
     assert big["worker_interleaved"] and "interleave" not in big["launch_kind"]
-    assert not pifft.dry_run(1 << 14, 8, 1, F64)["worker_interleaved"]          # single-pass local FFT
+    assert not pifft.dry_run(1 << 14, 16, 1, F64)["worker_interleaved"]         # single-pass local FFT
     assert not pifft.dry_run(1 << 20, 32, 1, F64)["worker_interleaved"]         # two tree launches
     assert not pifft.dry_run(1 << 20, 8, 1, F64, first=0, count=4)["worker_interleaved"]
     assert not pifft.dry_run(1 << 20, 1, 1, F64)["worker_interleaved"]

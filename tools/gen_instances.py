@@ -136,6 +136,11 @@ for T, prec in (("double", 64), ("float", 32)):
     for lp in (1, 2, 3, 4):
         for logm in range(10 - lp, min(14 - lp, 12)):  # (M < 4096: fp64 P = 2 at 4096 spills)
             items.append(f"PK({T}, {prec}, {1 << logm}, {1 << lp}, 11, 0, {lp}),")
+# (fp32 spills nowhere at M = 4096, P = 2: that one too.  16384-value
+# one-launch tiles -- 1024 threads, fp64 2^14 P = 8, fp32 2^14 P = 4 / 8 --
+# measured 14-16 vs 9-11 us, profiles/r05za_small_plan_edges.log: not
+# instantiated)
+items.append("PK(float, 32, 4096, 2, 11, 0, 1),")
 # (config 2's slice with its fused tree pass at C = 2 -- 128 workgroups
 # gathering leaves, 32-B leaf segments: +0.7 % on the slice, 0 to +2.4 % on
 # neighbouring slices, within run-to-run noise; round 4,
