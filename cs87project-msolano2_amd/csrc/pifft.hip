@@ -678,10 +678,13 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // PIFFT_WIL_SINGLE_MIN_LOG: the two-pass plan's smallest M, log2.  Tuning.)
     const uint64_t pm = (uint64_t)p->P * p->m;
     const int nts0 = pick_nts(2 * ntrans * p->m * esz);
-    const bool one_ok = wil_ok && passes.size() == 1 && pm >= 1024 &&
+    // (P = 32 too, one launch only: two threads per position, each evaluating
+    // the tree pruned to half the workers)
+    const bool wil_ok5 = p->natural && p->P > 1 && p->nq == p->P && p->lp == 5 && env_int("PIFFT_WORKER_IL", 1);
+    const bool one_ok = (wil_ok || wil_ok5) && passes.size() == 1 && pm >= 1024 &&
                         pm <= (uint64_t)env_int("PIFFT_WIL_ONE_MAX", 8192) && env_int("PIFFT_WIL_ONE_LAUNCH", 1) &&
                         find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp);
-    const bool wil_single = wil_ok && passes.size() == 1 && p->batch == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
+    const bool wil_single = (wil_ok || one_ok) && passes.size() == 1 && p->batch == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
                             (p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11)) || one_ok);
     if (wil_single) p->wil = true;
     // The worker-interleaved plan with its tree fused into the first pass
@@ -942,7 +945,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
             if (t.dst == -2) t.dst = BUF_OUT;
             p->tree_only.push_back(t);
         }
-        if (p->wil) {  // one launch over all workers (lp <= 4): the passes' interleaved layout
+        if (p->wil && p->lp <= 4) {  // one launch over all workers: the passes' interleaved layout
             static const void* tw64[5] = {nullptr, (const void*)&k_tree_wil<double, 1>, (const void*)&k_tree_wil<double, 2>,
                                           (const void*)&k_tree_wil<double, 3>, (const void*)&k_tree_wil<double, 4>};
             static const void* tw32[5] = {nullptr, (const void*)&k_tree_wil<float, 1>, (const void*)&k_tree_wil<float, 2>,

@@ -741,8 +741,6 @@ __device__ __forceinline__ void wil_tree_to_lds(const PassArgs& a, T* lds, cx<T>
     using St = Stage<R, C, 2, 0, VPT>;
     constexpr int P = 1 << LP, J = C / P;
     constexpr int NT = PassCfg<R, C, VPT>::NT;
-    constexpr int PPT = Sh::Q / P;  // tree positions per thread
-    static_assert(C % P == 0 && Sh::Q % P == 0 && PPT * P * NT == C * R, "MODE 11 tile: J P lines, Q / P positions");
     constexpr LdsLayout LL = LdsPick<T, R, C, 2, VPT>::value;
     const uint32_t log_lb = a.log_lb;
     const uint32_t lbi = log_lb + (uint32_t)LP;
@@ -751,6 +749,47 @@ __device__ __forceinline__ void wil_tree_to_lds(const PassArgs& a, T* lds, cx<T>
     const uint64_t bt = line0 >> lbi;
     const uint64_t j0 = (line0 & ((1ull << lbi) - 1)) >> LP;
     const C2* __restrict__ x = static_cast<const C2*>(a.in) + bt * a.in_bstride;
+    if constexpr (P > Sh::Q) {
+        // P = 2 Q (32 workers at 16 values per thread): two threads per
+        // position, thread half h evaluating the tree pruned to workers [h P/2,
+        // (h + 1) P/2) (tree_levels' worker range: the reference's order on
+        // the branches it keeps); h is uniform per wave from R = 64 on
+        static_assert(P == 2 * Sh::Q && 2 * J * R == NT, "MODE 11, P = 2Q: two threads per position");
+        constexpr int H = P / 2;
+        const int p = tid % (J * R), h = tid / (J * R);
+        const uint64_t i = j0 + (uint64_t)(p % J) + ((uint64_t)(p / J) << log_lb);
+        C2 w[P];
+#pragma unroll
+        for (int m = 0; m < P; m++) w[m] = ld_stream<nt_loads(NTS)>(x + i + ((uint64_t)m << log_m));
+        tree_levels<T, LP>(w, a.tree, i, log_m, 0, 0, 0, (uint64_t)(h * H), (uint64_t)(h * H + H));
+        const int jl = p % J, r = p / J;
+#pragma unroll
+        for (int comp = 0; comp < 2; comp++) {
+            if (comp) __syncthreads();
+            if (h) {
+#pragma unroll
+                for (int m = 0; m < H; m++) lds[lds_at(LL, jl * P + H + m, r)] = comp ? w[H + m].im : w[H + m].re;
+            } else {
+#pragma unroll
+                for (int m = 0; m < H; m++) lds[lds_at(LL, jl * P + m, r)] = comp ? w[m].im : w[m].re;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < St::U; u++) {
+                int c, b;
+                St::map(tid, u, c, b);
+#pragma unroll
+                for (int k = 0; k < St::q; k++) {
+                    const T y = lds[lds_at(LL, c, b + k * St::NB)];
+                    if (comp) v[u * St::q + k].im = y; else v[u * St::q + k].re = y;
+                }
+            }
+        }
+        __syncthreads();
+        return;
+    } else {
+    constexpr int PPT = Sh::Q / P;  // tree positions per thread
+    static_assert(C % P == 0 && Sh::Q % P == 0 && PPT * P * NT == C * R, "MODE 11 tile: J P lines, Q / P positions");
     C2 w[PPT][P];
 #pragma unroll
     for (int u = 0; u < PPT; u++) {  // every leaf load issued before any use
@@ -787,6 +826,7 @@ __device__ __forceinline__ void wil_tree_to_lds(const PassArgs& a, T* lds, cx<T>
         }
     }
     __syncthreads();  // every read done before the first stage's exchange writes LDS
+    }
 }
 
 #ifndef PIFFT_SERIAL_BFLY
@@ -1327,7 +1367,7 @@ constexpr int first_tw_count() {
 template <typename T, int R, int C, int MODE, int LP, int VPT>
 constexpr int pass_waves_per_eu() {
     constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
-    return ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
+    return ((MODE & 3) == 3 && LP >= 5) ? 1 : ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)

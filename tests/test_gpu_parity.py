@@ -872,22 +872,25 @@ def test_single_pass_all_worker_plans_two_pass(suf, logn, P, kinds, monkeypatch)
 
 @pytest.mark.parametrize("suf", ["f64", "f32"])
 @pytest.mark.parametrize("logn", [10, 11, 12, 13])
-@pytest.mark.parametrize("P", [2, 4, 8, 16])
+@pytest.mark.parametrize("P", [2, 4, 8, 16, 32])
 def test_tiny_all_worker_plans_one_launch(suf, logn, P, monkeypatch):
     """The reference's own GPU sweep grid (cuda/run-experiments:16-17: n =
-    1024-8192, p up to 16 here): one fused launch -- every worker's tree,
-    then its whole N/P-point FFT, natural-order store -- where N/P < 4096,
-    against the oracle and the three-launch plan."""
+    1024-8192, p up to 32): one fused launch -- every worker's tree, then its
+    whole N/P-point FFT, natural-order store -- where N/P < 4096 (P = 32: two
+    threads per position, each with half the workers' tree; fp64 up to 4096),
+    against the oracle and the three-launch (P = 32: four-launch) plan."""
     n = 1 << logn
     x = oracle.generate(n, DT[suf], seed=logn * 3 + P)
     plan = pifft.Plan(n, P, 1, PREC[suf])
     kinds = plan.describe()["launch_kind"]
-    assert kinds == (ONE if n // P < 4096 or (suf == "f32" and P == 2) else THREE), kinds
+    many = ["tree", "tree", "pass", "interleave"] if P == 32 else THREE
+    one = (n // P < 4096 or (suf == "f32" and P == 2)) and not (P == 32 and suf == "f64" and n == 8192)
+    assert kinds == (ONE if one else many), kinds
     got = run(plan, x)
     assert_bins_close(got, oracle.fft(x, P=1, nthreads=8), suf, n)
     monkeypatch.setenv("PIFFT_WIL_ONE_LAUNCH", "0")
     three = pifft.Plan(n, P, 1, PREC[suf])
-    assert three.describe()["launch_kind"] == THREE
+    assert three.describe()["launch_kind"] == many
     assert rel_l2(run(three, x), got) <= tol(suf, n)
 
 

@@ -100,7 +100,10 @@ def test_tiny_all_worker_plans_one_launch(monkeypatch):
             assert d["radix"] == [n // P] and d["lines"] == [P] and d["worker_interleaved"]
     assert pifft.dry_run(1 << 13, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]  # M = 4096
     assert pifft.dry_run(1 << 13, 2, 1, F32)["launch_kind"] == ["tree+pass"]                    # (spill-free)
-    assert pifft.dry_run(1 << 13, 32, 1, F64)["launch_kind"][-1] == "interleave"               # P = 32
+    assert pifft.dry_run(1 << 13, 32, 1, F64)["launch_kind"][-1] == "interleave"               # P = 32 fp64 8192
+    assert pifft.dry_run(1 << 12, 32, 1, F64)["launch_kind"] == ["tree+pass"]                   # ... 4096: one
+    assert pifft.dry_run(1 << 13, 32, 1, F32)["launch_kind"] == ["tree+pass"]
+    assert pifft.dry_run(1 << 14, 32, 1, F32)["launch_kind"][-1] == "interleave"
     assert pifft.dry_run(1 << 9, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]   # < 1024
     assert pifft.dry_run(1 << 12, 8, 2, F64)["launch_kind"][0] == "tree"                       # batched
     monkeypatch.setenv("PIFFT_WIL_ONE_LAUNCH", "0")

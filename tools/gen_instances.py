@@ -141,6 +141,11 @@ for T, prec in (("double", 64), ("float", 32)):
 # measured 14-16 vs 9-11 us, profiles/r05za_small_plan_edges.log: not
 # instantiated)
 items.append("PK(float, 32, 4096, 2, 11, 0, 1),")
+# P = 32 (two threads per position, one launch only): n = 1024-4096 fp64 (8192
+# spills), 1024-8192 fp32
+for T, prec, ms in (("double", 64, (32, 64, 128)), ("float", 32, (32, 64, 128, 256))):
+    for m in ms:
+        items.append(f"PK({T}, {prec}, {m}, 32, 11, 0, 5),")
 # (config 2's slice with its fused tree pass at C = 2 -- 128 workgroups
 # gathering leaves, 32-B leaf segments: +0.7 % on the slice, 0 to +2.4 % on
 # neighbouring slices, within run-to-run noise; round 4,
