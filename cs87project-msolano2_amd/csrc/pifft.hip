@@ -843,8 +843,11 @@ int build_plan(pifft_plan* p, bool dry = false) {
         if (p->log_n <= direct_max) {
             tree_is_direct = true;
             tree_direct = tb.reference_omega_levels(p->n, p->lp);
+            // (and at P = 32, whose one-launch pass evaluates 16 workers' tree
+            // per thread: 80 dependent table lookups each, against 5: 2^10
+            // 12 -> 8 us, fp32 11 -> 6; P = 16 ties, profiles/r05p32b_*)
             wil_factored = p->wil && env_int("PIFFT_WIL_TREE_DIRECT", 0) == 0 &&
-                           (uint64_t)p->batch * p->n >= (1ull << env_int("PIFFT_WIL_TREE_MIN_LOG", 21));
+                           ((uint64_t)p->batch * p->n >= (1ull << env_int("PIFFT_WIL_TREE_MIN_LOG", 21)) || p->lp == 5);
             if (wil_factored) tree2 = two_level(tb, p->n);
         } else {
             tree2 = two_level(tb, p->n);
