@@ -670,22 +670,25 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // reference's own GPU sweep, cuda/run-experiments:16) runs every worker's
     // tree and its whole M-point FFT in ONE launch: the fused pass at J = 1 (C
     // = P lines of R = M points) storing natural order (PIFFT_WIL_ONE_LAUNCH=0:
-    // off).
+    // off).  Batched, one workgroup per transform: 1.2-2.8x faster than tree +
+    // pass (profiles/r05bo_batched_one_launch_ab.log; PIFFT_WIL_ONE_BATCH=0: off).
     // The two-pass plan from M = 2^11 (fp64 2^14 P = 8 11 -> 10 us, fp32 8 vs
     // 11, fp32 2^15 P = 16 12 vs 14: profiles/r05za_small_plan_edges.log).
     // (PIFFT_WIL_ONE_MAX: the largest one-launch transform, values -- 16384
     // measured slower; the instances exist only where they compile spill-free.
     // PIFFT_WIL_SINGLE_MIN_LOG: the two-pass plan's smallest M, log2.  Tuning.)
     const uint64_t pm = (uint64_t)p->P * p->m;
-    const int nts0 = pick_nts(2 * ntrans * p->m * esz);
+    int nts0 = pick_nts(2 * ntrans * p->m * esz);
+    if (nts0 && !find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp)) nts0 = 0;  // (nt forms not instantiated)
     // (P = 32 too, one launch only: two threads per position, each evaluating
     // the tree pruned to half the workers)
     const bool wil_ok5 = p->natural && p->P > 1 && p->nq == p->P && p->lp == 5 && env_int("PIFFT_WORKER_IL", 1);
     const bool one_ok = (wil_ok || wil_ok5) && passes.size() == 1 && pm >= 1024 &&
                         pm <= (uint64_t)env_int("PIFFT_WIL_ONE_MAX", 8192) && env_int("PIFFT_WIL_ONE_LAUNCH", 1) &&
                         find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp);
-    const bool wil_single = (wil_ok || one_ok) && passes.size() == 1 && p->batch == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
-                            (p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11)) || one_ok);
+    const bool wil_single = (wil_ok || one_ok) && passes.size() == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
+                            ((p->batch == 1 && p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11))) ||
+                             (one_ok && (p->batch == 1 || env_int("PIFFT_WIL_ONE_BATCH", 1))));
     if (wil_single) p->wil = true;
     // The worker-interleaved plan with its tree fused into the first pass
     // (MODE 11, k_pass wil_tree_to_lds): a tile of J adjacent line indices x

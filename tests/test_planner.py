@@ -92,7 +92,8 @@ def test_tiny_all_worker_plans_one_launch(monkeypatch):
     """A single transform of P M <= 8192 values (from 1024, M < 4096 but fp32 P = 2: the
     reference's GPU sweep sizes) runs as ONE fused pass: J = 1, C = P lines
     of R = M points, every worker's tree then its whole local FFT, storing
-    natural order."""
+    natural order; batched, one workgroup per transform (profiles/
+    r05bo_batched_one_launch_ab.log: 1.2-2.8x)."""
     for prec in (F64, F32):
         for n, P in ((1 << 10, 2), (1 << 10, 16), (1 << 12, 8), (1 << 13, 4), (1 << 13, 16)):
             d = pifft.dry_run(n, P, 1, prec)
@@ -105,7 +106,8 @@ def test_tiny_all_worker_plans_one_launch(monkeypatch):
     assert pifft.dry_run(1 << 13, 32, 1, F32)["launch_kind"] == ["tree+pass"]
     assert pifft.dry_run(1 << 14, 32, 1, F32)["launch_kind"][-1] == "interleave"
     assert pifft.dry_run(1 << 9, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]   # < 1024
-    assert pifft.dry_run(1 << 12, 8, 2, F64)["launch_kind"][0] == "tree"                       # batched
+    assert pifft.dry_run(1 << 12, 8, 2, F64)["launch_kind"] == ["tree+pass"]                   # batched too
+    assert pifft.dry_run(4096, 4, 4096, F32)["launch_kind"] == ["tree+pass"]                    # one workgroup each
     monkeypatch.setenv("PIFFT_WIL_ONE_LAUNCH", "0")
     assert pifft.dry_run(1 << 12, 8, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]
 
