@@ -671,7 +671,9 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // tree and its whole M-point FFT in ONE launch: the fused pass at J = 1 (C
     // = P lines of R = M points) storing natural order (PIFFT_WIL_ONE_LAUNCH=0:
     // off).  Batched, one workgroup per transform: 1.2-2.8x faster than tree +
-    // pass (profiles/r05bo_batched_one_launch_ab.log; PIFFT_WIL_ONE_BATCH=0: off).
+    // pass (profiles/r05bo_batched_one_launch_ab.log; PIFFT_WIL_ONE_BATCH=0: off);
+    // and batched two-pass plans 11-40 % (r05bt_batched_two_pass_ab.log;
+    // PIFFT_WIL_SINGLE_BATCH=0: off).
     // The two-pass plan from M = 2^11 (fp64 2^14 P = 8 11 -> 10 us, fp32 8 vs
     // 11, fp32 2^15 P = 16 12 vs 14: profiles/r05za_small_plan_edges.log).
     // (PIFFT_WIL_ONE_MAX: the largest one-launch transform, values -- 16384
@@ -687,7 +689,8 @@ int build_plan(pifft_plan* p, bool dry = false) {
                         pm <= (uint64_t)env_int("PIFFT_WIL_ONE_MAX", 8192) && env_int("PIFFT_WIL_ONE_LAUNCH", 1) &&
                         find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp);
     const bool wil_single = (wil_ok || one_ok) && passes.size() == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
-                            ((p->batch == 1 && p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11))) ||
+                            (((p->batch == 1 || env_int("PIFFT_WIL_SINGLE_BATCH", 1)) &&
+                              p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11))) ||
                              (one_ok && (p->batch == 1 || env_int("PIFFT_WIL_ONE_BATCH", 1))));
     if (wil_single) p->wil = true;
     // The worker-interleaved plan with its tree fused into the first pass
@@ -776,7 +779,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
         // plan after its tree launch still saves the interleave launch (2^16
         // 16 -> 15 us, 2^17 21 -> 16, 2^18 30 -> 19; r05w_small_wil.log)
         std::vector<PassChoice> w;
-        p->wil = p->lp == 4 && p->m >= 4096 && plan_passes(p->m, p->prec, ntrans, w, 0, false, false, ilog2u(p->m) - 1) == 0 &&
+        p->wil = p->lp == 4 && p->batch == 1 && p->m >= 4096 && plan_passes(p->m, p->prec, ntrans, w, 0, false, false, ilog2u(p->m) - 1) == 0 &&
                  w.size() == 2 && to_wil(w);
         if (p->wil) passes = w;
     }

@@ -71,7 +71,7 @@ def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
     pass -- two launches instead of tree + pass + interleave -- from M = 2^12
     up (2^11 at the fused plans) where that plan exists; fp64 P = 16 (no fused pass there) the
     worker-interleaved two-pass plan after its tree launch (profiles/
-    r05w_small_wil.log).  Batched plans and M < 2^12 keep the single pass."""
+    r05w_small_wil.log; batched: r05bt_batched_two_pass_ab.log).  M < 2^11 keeps the single pass."""
     def kinds(n, P, prec, b=1):
         return pifft.dry_run(n, P, b, prec)["launch_kind"]
     assert kinds(1 << 17, 8, F64) == ["tree+pass", "pass"]
@@ -83,7 +83,8 @@ def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
     assert kinds(1 << 14, 8, F64) == ["tree+pass", "pass"]               # M = 2^11
     assert kinds(1 << 14, 16, F64) == ["tree", "pass", "interleave"]    # M = 2^10
     assert kinds(1 << 15, 16, F64) == ["tree", "pass", "interleave"]
-    assert kinds(1 << 15, 4, F64, b=4) == ["tree", "pass", "interleave"]  # batched
+    assert kinds(1 << 15, 4, F64, b=4) == ["tree+pass", "pass"]           # batched too (r05bt)
+    assert kinds(1 << 18, 16, F64, b=2) == ["tree", "pass", "interleave"]  # (fp64 P = 16's two-pass: batch 1 only)
     monkeypatch.setenv("PIFFT_WIL_SINGLE", "0")
     assert kinds(1 << 17, 8, F64) == ["tree", "pass", "interleave"]
 
