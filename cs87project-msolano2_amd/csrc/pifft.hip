@@ -745,6 +745,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
             } else if (rest8 > (p->prec == 64 ? 2048u : 1024u) && rest4 <= 2048 && (p->prec == 64 || p->lp == 3)) {
                 J = 4;
             }
+        } else if (jdef == 8 && p->lp == 4) {
+            // fp32 P = 16: J = 4 where it leaves a remainder of at most 1024
+            // points (2^21: 41 -> 26 us; at 2048 its 4-line pass loses, 2^22
+            // 52 -> 90, r05u_wil_fuse_remainder.log)
+            const uint64_t rest8 = p->m / (uint64_t)(tile1 / (8 << p->lp));
+            if (rest8 > 1024 && rest8 / 2 <= 1024) J = 4;
+        } else if (jdef == 0 && p->lp == 4 && p->prec == 64 && data >= (32ull << 20) && data <= (64ull << 20)) {
+            J = 2;  // fp64 P = 16 at 32-64 MiB: fused at J = 2 (2^21 43 -> 37 us, 2^22 70 -> 65; 2^23 loses)
         }
         const int jenv = env_int("PIFFT_WIL_FUSE_J", -1);
         if (jenv >= 0) {

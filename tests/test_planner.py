@@ -40,7 +40,8 @@ def test_fused_all_worker_rule():
     assert first(1 << 21, 8, F64) == (11, 128, 64)     # fp64 P <= 8: J = 8
     assert first(1 << 28, 8, F64) == (11, 128, 64)
     assert first(1 << 21, 2, F64) == (11, 512, 16)
-    assert first(1 << 22, 16, F64)[0] == 0               # fp64 P = 16 below 256 MiB: the tree launch
+    assert first(1 << 23, 16, F64)[0] == 0               # fp64 P = 16 below 256 MiB: the tree launch
+    assert first(1 << 22, 16, F64) == (11, 256, 32)     # ... but J = 2 at 32-64 MiB
     assert first(1 << 28, 16, F64) == (11, 64, 128)     # ... and from 256 MiB fused
     assert first(1 << 21, 2, F32) == (11, 512, 16)      # fp32 up to 32 MiB: J = 8
     assert first(1 << 24, 8, F32) == (11, 64, 128)      # up to 1 GiB: J = 16
@@ -62,7 +63,10 @@ def test_fused_all_worker_rule():
     assert pifft.dry_run(1 << 21, 8, 1, F32)["radix"] == [256, 1024]
     assert pifft.dry_run(1 << 22, 8, 1, F32)["radix"] == [256, 2048]
     assert pifft.dry_run(1 << 22, 4, 1, F32)["radix"] == [256, 64, 64]  # fp32 P = 4 keeps J = 8
-    assert pifft.dry_run(1 << 22, 16, 1, F32)["lines"][0] == 128        # ... and P = 16
+    assert pifft.dry_run(1 << 22, 16, 1, F32)["lines"][0] == 128        # ... and P = 16 at 2^22
+    assert pifft.dry_run(1 << 21, 16, 1, F32)["radix"] == [128, 1024]   # (P = 16 fp32: a 1024-point remainder)
+    assert pifft.dry_run(1 << 21, 16, 1, F64)["lines"][0] == 32         # fp64 P = 16 at 32-64 MiB: J = 2
+    assert pifft.dry_run(1 << 23, 16, 1, F64)["launch_kind"][0] == "tree"
 
 
 def test_single_pass_all_worker_plans_go_worker_interleaved(monkeypatch):
