@@ -681,13 +681,16 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // PIFFT_WIL_SINGLE_MIN_LOG: the two-pass plan's smallest M, log2.  Tuning.)
     const uint64_t pm = (uint64_t)p->P * p->m;
     int nts0 = pick_nts(2 * ntrans * p->m * esz);
-    if (nts0 && !find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp)) nts0 = 0;  // (nt forms not instantiated)
+    // (fp64 P = 2 at M = 4096 spills at 16 values per thread: 8, 1024 threads,
+    // batched only -- 64 transforms 21 -> 13 us, one 10 -> 12: profiles/r05v8_*)
+    const int vpt0 = find_pass(p->prec, (int)p->m, (int)p->P, 11, 0, p->lp) ? 16 : p->batch >= 64 ? 8 : 0;
+    if (nts0 && !find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp, vpt0)) nts0 = 0;  // (nt forms not instantiated)
     // (P = 32 too, one launch only: two threads per position, each evaluating
     // the tree pruned to half the workers)
     const bool wil_ok5 = p->natural && p->P > 1 && p->nq == p->P && p->lp == 5 && env_int("PIFFT_WORKER_IL", 1);
     const bool one_ok = (wil_ok || wil_ok5) && passes.size() == 1 && pm >= 1024 &&
                         pm <= (uint64_t)env_int("PIFFT_WIL_ONE_MAX", 8192) && env_int("PIFFT_WIL_ONE_LAUNCH", 1) &&
-                        find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp);
+                        find_pass(p->prec, (int)p->m, (int)p->P, 11, nts0, p->lp, vpt0);
     const bool wil_single = (wil_ok || one_ok) && passes.size() == 1 && env_int("PIFFT_WIL_SINGLE", 1) &&
                             (((p->batch == 1 || env_int("PIFFT_WIL_SINGLE_BATCH", 1)) &&
                               p->m >= (1ull << env_int("PIFFT_WIL_SINGLE_MIN_LOG", 11))) ||
@@ -729,7 +732,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     // (values), PIFFT_WIL_FUSE_VPT: values per thread (tuning, tests).
     uint32_t wil_fused_c = 0;
     if (wil_single && one_ok && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {
-        passes = {PassChoice{(int)p->m, (int)p->P, 11, nts0}};
+        passes = {PassChoice{(int)p->m, (int)p->P, 11, nts0, vpt0}};
         wil_fused_c = p->P;
     }
     if (p->wil && !wil_fused_c && !p->separate_tree && env_int("PIFFT_WIL_FUSE", 1)) {

@@ -815,7 +815,8 @@ def test_worker_interleaved_layout_vs_slice_major(suf, logn, P, batch, monkeypat
                                                 ("f64", 17, 4, 1, 0), ("f32", 18, 8, 2, 0), ("f64", 17, 8, 1, 0),
                                                 ("f64", 14, 2, 1, 0), ("f64", 15, 4, 1, 0), ("f32", 16, 16, 1, 0),
                                                 ("f32", 16, 8, 1, 0), ("f32", 12, 4, 3, 0), ("f64", 11, 8, 5, 0),
-                                                ("f64", 12, 32, 2, 0), ("f32", 10, 2, 7, 0), ("f64", 15, 4, 3, 0),
+                                                ("f64", 12, 32, 2, 0), ("f32", 10, 2, 7, 0), ("f64", 13, 2, 64, 0),
+                                                ("f64", 15, 4, 3, 0),
                                                 ("f32", 14, 8, 5, 0), ("f32", 21, 16, 1, 0), ("f64", 21, 16, 1, 0)])
 def test_fused_all_worker_tree_pass(suf, logn, P, batch, j, monkeypatch):
     """All-worker natural-order plans with every worker's tree fused into the

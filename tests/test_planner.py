@@ -104,8 +104,9 @@ def test_tiny_all_worker_plans_one_launch(monkeypatch):
             d = pifft.dry_run(n, P, 1, prec)
             assert d["launch_kind"] == ["tree+pass"] and d["launch_mode"] == [11], (n, P, d)
             assert d["radix"] == [n // P] and d["lines"] == [P] and d["worker_interleaved"]
-    assert pifft.dry_run(1 << 13, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]  # M = 4096
-    assert pifft.dry_run(1 << 13, 2, 1, F32)["launch_kind"] == ["tree+pass"]                    # (spill-free)
+    assert pifft.dry_run(1 << 13, 2, 1, F64)["launch_kind"] == ["tree", "pass", "interleave"]  # M = 4096 ...
+    assert pifft.dry_run(1 << 13, 2, 64, F64)["vpt"] == [8]                                    # ... batched: 8 per thread
+    assert pifft.dry_run(1 << 13, 2, 1, F32)["launch_kind"] == ["tree+pass"]                    # (spill-free at 16)
     assert pifft.dry_run(1 << 13, 32, 1, F64)["launch_kind"][-1] == "interleave"               # P = 32 fp64 8192
     assert pifft.dry_run(1 << 12, 32, 1, F64)["launch_kind"] == ["tree+pass"]                   # ... 4096: one
     assert pifft.dry_run(1 << 13, 32, 1, F32)["launch_kind"] == ["tree+pass"]

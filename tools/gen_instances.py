@@ -143,6 +143,7 @@ for T, prec in (("double", 64), ("float", 32)):
 # measured 14-16 vs 9-11 us, profiles/r05za_small_plan_edges.log: not
 # instantiated)
 items.append("PK(float, 32, 4096, 2, 11, 0, 1),")
+items.append("PKV(double, 64, 4096, 2, 11, 0, 1, 8),")  # fp64 P = 2 at 8192 values: 8 per thread, spill-free
 # P = 32 (two threads per position, one launch only): n = 1024-4096 fp64 (8192
 # spills), 1024-8192 fp32
 for T, prec, ms in (("double", 64, (32, 64, 128)), ("float", 32, (32, 64, 128, 256))):
