@@ -656,16 +656,19 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
 
 def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, red_dev) -> dict:
     """Configs 2 and 3 on a multi-GPU job, each a timed loop with the headline's
-    barrier + max-over-ranks contract: C2 split one worker per GPU (the
-    reference's 8-way split on real GPUs, P = world), C3's 4096 transforms
-    sharded by transform over the GPUs.  Rank 0's dominant-kernel roofline
-    comes from the same loop."""
+    barrier + max-over-ranks contract: C2's 8 workers split over the GPUs
+    (the reference's 8-way split on real GPUs: one worker per GPU at 8, 8/G
+    at G = 1, 2, 4), C3's 4096 transforms sharded by transform over the GPUs.
+    Rank 0's dominant-kernel roofline comes from the same loop; the worker
+    split checks itself (exchange_and_verify, at one rank too)."""
     import pifft_dist
     F64, F32 = pifft.F64, pifft.F32
     b0, bc = pifft_dist.batch_range(rank, world, 4096)
+    p2 = 8 if 8 % world == 0 else world
+    f2, c2 = pifft_dist.worker_range(rank, world, p2)
     cases = [
-        ("C2_split", f"config 2: fp64 N=2^20 split over {world} GPUs, one worker each (slice-major; "
-                     f"no data-path collective)", 20, F64, dict(P=world, first=rank, count=1, batch_local=1, b_first=0), 1),
+        ("C2_split", f"config 2: fp64 N=2^20, {p2} workers split over {world} GPU(s), {c2} each (no data-path "
+                     f"collective)", 20, F64, dict(P=p2, first=f2, count=c2, batch_local=1, b_first=0), 1),
         ("C3_batch", f"config 3: batched fp32 4096 x N=4096 sharded by transform over {world} GPUs",
          12, F32, dict(P=1, first=0, count=1, batch_local=bc, b_first=b0), 4096),
     ]
@@ -683,7 +686,7 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
                         "unit": "GFLOP/s", "ms_per_step": round(ms, 6), "steps": k, "n_gpus": world,
                         "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"],
                         "roofline_rank0": job.roofline(local_s * 1e3 / k) if rank == 0 else None})
-            if g["count"] < g["P"]:  # a worker split: check it (slices bitwise, gathered result vs one GPU)
+            if key == "C2_split":  # a worker split: check it (slices bitwise, gathered result vs one GPU)
                 exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, rec)
             job.free()
         except Exception as e:  # reported, never silently replaced
@@ -838,6 +841,8 @@ def allgather(pifft, torch, dist, job, barrier, red_dev, keep: bool = False):
         gathered = pifft_dist.slices_transform_major(gathered, world, batch)
         natural = torch.empty(job.n * batch, dtype=job.y.dtype, device=job.dev)
         pifft.interleave_device(gathered.data_ptr(), natural.data_ptr(), job.n, job.P, batch, job.prec, job.stream)
+    elif keep:
+        natural = gathered.reshape(-1)  # whole transforms in natural order (a world-size-1 group: its own result)
     torch.cuda.synchronize(job.dev)
     ms = pifft_dist.max_over_ranks((time.perf_counter() - ta) * 1e3, red_dev)
     del gathered
@@ -853,10 +858,10 @@ def allgather(pifft, torch, dist, job, barrier, red_dev, keep: bool = False):
 LINE_MAX_CHARS = 7000
 
 _RF_KEYS = ("bound", "kernel_name", "launches", "mean_ms", "loop_reps", "trace_loop_dispatches", "achieved",
-            "peak", "unit", "frac", "traffic", "algorithmic_bytes", "kernel_ms_per_step", "all_launches_ms_per_step",
+            "peak", "unit", "frac", "traffic", "traffic_source", "algorithmic_bytes", "kernel_ms_per_step", "all_launches_ms_per_step",
             "step_ms", "step_frac", "checks", "error")
 _RF_SECONDARY = ("kernel_name", "launches", "mean_ms", "loop_reps", "trace_loop_dispatches", "achieved", "peak",
-                 "frac", "traffic", "algorithmic_bytes", "step_frac", "error")
+                 "frac", "traffic", "traffic_source", "algorithmic_bytes", "step_frac", "error")
 _CPU_KEYS = ("value", "unit", "cores", "kind", "ms", "sample", "cpu_model", "cpu_share", "error")
 
 
@@ -959,9 +964,10 @@ def guarded(rec: dict, key: str, fn, *a, **kw):
 
 
 def _fault(stage: str, rank: int) -> None:
-    """Test-only fault injection (BENCH_FAULT=<stage>[:rank]): raises in that
-    stage on that rank (default rank 0), to check that the line survives."""
-    spec = os.environ.get("BENCH_FAULT", "")
+    """Test-only fault injection (BENCH_FAULT=<stage>[:rank], read only under
+    PIFFT_TUNING=1 like libpifft's PIFFT_FAULT): raises in that stage on that
+    rank (default rank 0), to check that the line survives."""
+    spec = os.environ.get("BENCH_FAULT", "") if os.environ.get("PIFFT_TUNING") == "1" else ""
     if not spec:
         return
     st, _, r = spec.partition(":")
@@ -996,6 +1002,10 @@ def main() -> int:
                     help="reference pthreads for the CPU baseline (default: the reference's own p_to = 32, "
                          "within the online CPUs and host memory)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo")
+    ap.add_argument("--pg", action="store_true",
+                    help="open the process group even at one rank (with --dist-backend nccl: a world-size-1 RCCL "
+                         "group on one GPU runs the multi-GPU code path -- init, barrier, device all-reduce, "
+                         "all_gather_object, the all-gather and the self-check -- before any multi-GPU job does)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (use with --dist-backend gloo)")
     ap.add_argument("--as-rank", default="",
@@ -1008,9 +1018,9 @@ def main() -> int:
     args = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
-    if world_env is None and args.gpus > 1:
+    if world_env is None and (args.gpus > 1 or args.pg):
         if args.as_rank:
-            raise SystemExit("--as-rank emulates one rank on one GPU: use it without --gpus")
+            raise SystemExit("--as-rank emulates one rank on one GPU: use it without --gpus or --pg")
         return spawn_ranks(args.gpus)
     world = int(world_env or "1")
     if world != args.gpus:
@@ -1024,8 +1034,8 @@ def main() -> int:
 
     emulated = None
     if args.as_rank:
-        if world > 1:
-            raise SystemExit("--as-rank is a single-process option")
+        if world > 1 or args.pg:
+            raise SystemExit("--as-rank is a single-process option without a process group")
         emulated = tuple(int(v) for v in args.as_rank.split("/"))
         if len(emulated) != 2 or not 0 <= emulated[0] < emulated[1]:
             raise SystemExit("--as-rank wants q/G with 0 <= q < G")
@@ -1036,7 +1046,7 @@ def main() -> int:
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
-    if world > 1:
+    if world > 1 or args.pg:
         import datetime
         import torch.distributed as dist
         # fail fast: a stuck collective on a first multi-GPU run ends in 3 min,
@@ -1149,16 +1159,16 @@ def main() -> int:
 
     # the optional exchange and the split's self-check (exchange_and_verify:
     # every failure an *_error field, all ranks on the same branch)
-    if dist is not None and (args.shard == "batch" or count < P):
+    if dist is not None and (args.shard == "batch" or count < P or world == 1):
         exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, cfg,
-                            verify=args.shard == "workers" and count < P, gather=args.allgather)
+                            verify=args.shard == "workers" and (count < P or world == 1), gather=args.allgather)
     job.free()
 
     if not args.no_secondary and not emulated:
-        if world == 1 and args.log_n == 28 and args.prec == 64 and args.batch == 1:
+        if dist is None and args.log_n == 28 and args.prec == 64 and args.batch == 1:
             cfg["secondary"] = secondary_configs(pifft, torch, gpu, args.steps, args.warmup, args.seed,
                                                  args.cpu_threads, not args.no_cpu_baseline)
-        elif world > 1 and args.shard == "workers":
+        elif dist is not None and args.shard == "workers":
             sec = guarded(cfg, "secondary_error", multi_secondary, pifft, torch, dist, gpu, rank, world,
                           args.steps, args.warmup, args.seed, barrier, red_dev)
             if sec is not None and world == 8:  # (config5 refuses cleanly when the HBM cannot hold it)

@@ -33,6 +33,8 @@
 #include <cxxabi.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -79,7 +81,21 @@ int env_int(const char* name, int dflt) {
 bool fault_at(const char* site) {
     if (!tuning_on()) return false;
     const char* s = getenv("PIFFT_FAULT");
-    return s && !strcmp(s, site);
+    const size_t n = strlen(site);
+    if (!s || strncmp(s, site, n)) return false;
+    if (s[n] == '\0') return true;  // <site>: every time it is reached
+    if (s[n] != ':') return false;
+    // <site>:K -- only the K-th time it is reached under this setting (e.g.
+    // peer_copy:3 fails the third copy, after two were enqueued)
+    static std::mutex mu;
+    static std::string last;
+    static long count = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    if (last != s) {
+        last = s;
+        count = 0;
+    }
+    return ++count == atol(s + n + 1);
 }
 
 // Timing events only time (pifft_execute_device_timed, pifft_profile_*,
@@ -135,10 +151,23 @@ const std::vector<PassKernel>& pass_kernels() {
     return all;
 }
 
+// every instance find_pass has returned in this process (pifft_instance_found):
+// the planner probes instances to choose between plans, so the instances a
+// plan depends on are those it found, launched or not (tests/test_instances.py)
+std::atomic<unsigned char>* found_log() {
+    static std::atomic<unsigned char>* f = new std::atomic<unsigned char>[pass_kernels().size()]();
+    return f;
+}
+
 const PassKernel* find_pass(int prec, int R, int C, int mode, int nts = 0, int lp = 0, int vpt = 16) {
-    for (const auto& k : pass_kernels())
-        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt)
+    const auto& all = pass_kernels();
+    for (size_t i = 0; i < all.size(); i++) {
+        const PassKernel& k = all[i];
+        if (k.prec == prec && k.R == R && k.C == C && k.mode == mode && k.nts == nts && k.lp == lp && k.vpt == vpt) {
+            found_log()[i].store(1, std::memory_order_relaxed);  // (plans may be built on several host threads)
             return &k;
+        }
+    }
     return nullptr;
 }
 
@@ -197,7 +226,6 @@ struct pifft_plan {
     void* d_hin = nullptr;   // pifft_execute's staging copies
     void* d_hout = nullptr;
     void* d_gather = nullptr;  // pifft_allgather: every worker's slices on this plan's device
-    void* d_nat = nullptr;  // pifft_execute_group: the gathered natural-order result (d_hin keeps the input)
     std::vector<char> host_tmp;
     std::vector<int> peer_on;  // devices this plan's device has peer access to (pifft_allgather)
     std::vector<hipStream_t> gst;  // pifft_allgather: one copy stream per source plan
@@ -224,10 +252,17 @@ struct DeviceGuard {
 struct TableBuilder {
     std::vector<char> blob;
     size_t esz;
+    bool size_only = false;  // a dry run: the blob's layout and size only (no memory, no values)
+    size_t sized = 0;        // the blob's size in a size_only run
     explicit TableBuilder(size_t e) : esz(e) {}
+    size_t size() const { return size_only ? sized : blob.size(); }
+    void grow_to(size_t bytes) {
+        if (size_only) sized = bytes;
+        else blob.resize(bytes);
+    }
     size_t align() {
-        size_t off = (blob.size() + 255) & ~(size_t)255;
-        blob.resize(off);
+        size_t off = (size() + 255) & ~(size_t)255;
+        grow_to(off);
         return off;
     }
     void put(double re, double im) {
@@ -244,6 +279,10 @@ struct TableBuilder {
     // w_L^(e*stride), e < count, accurate (long double) -- the Stockham tables
     size_t roots(uint64_t L, uint64_t count, uint64_t stride) {
         size_t off = align();
+        if (size_only) {
+            grow_to(off + count * esz);
+            return off;
+        }
         const long double two_pi = 6.283185307179586476925286766559005768L;
         for (uint64_t e = 0; e < count; e++) {
             const uint64_t x = (e * stride) % L;
@@ -257,6 +296,10 @@ struct TableBuilder {
     // k < N >> (t+1), at N - (N >> t) + k (level 0 = every k < N/2)
     size_t reference_omega_levels(uint64_t N, int levels) {
         size_t off = align();
+        if (size_only) {
+            grow_to(off + (N - (N >> (levels > 0 ? levels : 1))) * esz);
+            return off;
+        }
         // gcc -O1 and up folds the reference's cos()/sin() pair into one glibc
         // sincos() call; glibc's sincos and its separate cos/sin disagree in
         // the last fp64 bit for ~1e-3 of the angles (43 of 2^15 at N=2^16).
@@ -588,7 +631,6 @@ void release(pifft_plan* p) {
     if (p->d_hin) (void)hipFree(p->d_hin);
     if (p->d_hout) (void)hipFree(p->d_hout);
     if (p->d_gather) (void)hipFree(p->d_gather);
-    if (p->d_nat) (void)hipFree(p->d_nat);
     for (auto st : p->gst) (void)hipStreamDestroy(st);
     for (auto e : p->gdone) (void)hipEventDestroy(e);
     for (auto e : p->gev)
@@ -835,6 +877,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     }
     if (p->ilv) passes.back().nts = 0;
     TableBuilder tb(esz);
+    tb.size_only = dry;
     // --- tree tables (w_N) ---
     const bool need_tree = p->P > 1;
     size_t tree_direct = 0;
@@ -881,7 +924,7 @@ int build_plan(pifft_plan* p, bool dry = false) {
     TwoLevel pass2;
     if (passes.size() > 1) pass2 = two_level(tb, p->m);  // (every worker-interleaved plan has >= 2 passes)
     tb.align();
-    p->tw_bytes = tb.blob.size() ? tb.blob.size() : 256;
+    p->tw_bytes = tb.size() ? tb.size() : 256;
     if (!dry) {
         HIPCHK(hipMalloc(&p->d_tw, p->tw_bytes));
         if (!tb.blob.empty()) HIPCHK(hipMemcpy(p->d_tw, tb.blob.data(), tb.blob.size(), hipMemcpyHostToDevice));
@@ -1547,6 +1590,37 @@ int pifft_plan_dry_run(uint64_t n, uint32_t workers, uint32_t first, uint32_t co
     return rc;
 }
 
+int pifft_instance_count(void) { return (int)pass_kernels().size(); }
+
+int pifft_instance_desc(int i, int32_t* desc) {
+    if (!desc) return fail("desc is NULL");
+    if (i < 0 || i >= (int)pass_kernels().size()) return fail("instance %d out of range", i);
+    const PassKernel& k = pass_kernels()[(size_t)i];
+    const int32_t d[7] = {k.prec, k.R, k.C, k.mode, k.nts, k.lp, k.vpt};
+    memcpy(desc, d, sizeof d);
+    return 0;
+}
+
+int pifft_instance_found(int i) {
+    if (i < 0 || i >= (int)pass_kernels().size()) return fail("instance %d out of range", i);
+    return found_log()[(size_t)i].load(std::memory_order_relaxed);
+}
+
+int pifft_plan_dry_run_instances(uint64_t n, uint32_t workers, uint32_t first, uint32_t count, uint32_t batch,
+                                 int prec, int flags, int32_t* ids, int max_ids) {
+    if (!ids && max_ids > 0) return fail("ids is NULL");
+    pifft_plan* p = nullptr;
+    if (create(&p, n, workers, first, count, batch, prec, -1, flags, true)) return -1;
+    const int nl = (int)p->steps.size();
+    const PassKernel* base = pass_kernels().data();
+    for (int i = 0; i < nl && i < max_ids; i++) {
+        const PassKernel* k = p->steps[(size_t)i].pk;
+        ids[i] = k ? (int32_t)(k - base) : -1;
+    }
+    release(p);
+    return nl;
+}
+
 int pifft_plan_get_info(const pifft_plan* p, pifft_plan_info* info) {
     if (!p || !info) return fail("NULL argument");
     memset(info, 0, sizeof *info);
@@ -1652,8 +1726,9 @@ int pifft_launch_loop(pifft_plan* p, const int* launches, int nlaunches, int rep
 // Diagnostics build only (-DPIFFT_WG_CLOCK, tools/wg_clock.py; not in
 // include/pifft.h): `warm` full executions, then launches 0 .. launch-1 as
 // usual and `launch` with every workgroup recording its entry and
-// stores-done wall clock and hardware id (3 words per workgroup) into
-// host[0 .. min(3 grid, max_words)).  Returns the workgroup count (or -1);
+// stores-done wall clock, hardware id and per-stage stamps
+// (PIFFT_WGC_WORDS words per workgroup, PassArgs::wg_clock) into
+// host[0 .. min(PIFFT_WGC_WORDS grid, max_words)).  Returns the workgroup count (or -1);
 // *wall_hz = the wall clock's rate.  Synchronous.
 int pifft_debug_wg_clock(pifft_plan* p, int launch, const void* d_in, void* d_out, void* stream, int warm,
                          unsigned long long* host, size_t max_words, unsigned long long* wall_hz) {
@@ -1663,9 +1738,10 @@ int pifft_debug_wg_clock(pifft_plan* p, int launch, const void* d_in, void* d_ou
     if (s.kind != STEP_PASS && s.kind != STEP_TREE_PASS) return fail("launch %d is not a pass", launch);
     DeviceGuard g(p->device);
     hipStream_t st = (hipStream_t)stream;
-    const size_t nwg = (size_t)s.grid.x * s.grid.y * s.grid.z, words = 3 * nwg;
+    const size_t nwg = (size_t)s.grid.x * s.grid.y * s.grid.z, words = PIFFT_WGC_WORDS * nwg;
     unsigned long long* clk = nullptr;
     HIPCHK(hipMalloc(&clk, words * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(clk, 0, words * sizeof(unsigned long long)));  // (stamps a pass does not reach stay 0)
     int rc = 0;
     for (int k = 0; k < warm && rc == 0; k++) rc = launch_steps(p, d_in, d_out, st, nullptr);
     for (int i = 0; i < launch && rc == 0; i++) rc = launch_step(p, p->steps[(size_t)i], d_in, d_out, st);
@@ -1902,23 +1978,30 @@ int pifft_execute_group(pifft_plan** plans, int np, const void* host_in, void* h
     if (host_out) {
         if (np > 1 && check_cover(plans, np, true) == 0) {
             // the whole transform over several plans: gather on the first
-            // plan's device (pifft_allgather) into a plan-owned result
-            // buffer -- not the input staging copy, which
-            // pifft_execute_group_kernel_times re-runs the plans on -- and
-            // copy back once
+            // plan's device (pifft_allgather) into a result buffer held for
+            // this call only -- not the input staging copy, which
+            // pifft_execute_group_kernel_times re-runs the plans on, and not
+            // a persistent one (it would add N to the first device's
+            // footprint for the plan's life) -- and copy back once
             pifft_plan* p = plans[0];
+            const size_t nat_bytes = (size_t)p->batch * p->n * p->esz;
+            void* d_nat = nullptr;
             {
                 DeviceGuard g(p->device);
-                if (!p->d_nat) HIPCHK(hipMalloc(&p->d_nat, (size_t)p->batch * p->n * p->esz));
+                HIPCHK(hipMalloc(&d_nat, nat_bytes));
             }
             std::vector<const void*> sl(np);
             std::vector<void*> nat(np, nullptr);
             for (int i = 0; i < np; i++) sl[i] = plans[i]->d_hout;
-            nat[0] = p->d_nat;
-            if (gather_group(plans, np, sl.data(), nat.data(), nullptr)) return -1;
+            nat[0] = d_nat;
+            int rc = gather_group(plans, np, sl.data(), nat.data(), nullptr);
             DeviceGuard g(p->device);
-            HIPCHK(hipMemcpy(host_out, p->d_nat, (size_t)p->batch * p->n * p->esz, hipMemcpyDeviceToHost));
-            return 0;
+            if (rc == 0) {
+                const hipError_t e = hipMemcpy(host_out, d_nat, nat_bytes, hipMemcpyDeviceToHost);
+                if (e != hipSuccess) rc = fail("hipMemcpy of the gathered result: %s", hipGetErrorString(e));
+            }
+            (void)hipFree(d_nat);  // (synchronizes: no gather copy still writes it)
+            return rc;
         }
         for (int i = 0; i < np; i++) {
             pifft_plan* p = plans[i];

@@ -288,6 +288,43 @@ __device__ __forceinline__ cx<T> tree_tw_lv(const TreeTw& tw, uint64_t k, uint32
     return tree_tw<T>(tw, k << t);
 }
 
+// The twiddles tree_levels applies, fetched in one go before any of them is
+// used (round 6): with the reference-formula table, level tl's H = V >> (tl+1)
+// entries omega(N, (i + ml D) 2^t) (the same for every block of the level) at
+// w[V - (V >> tl) + ml]; with the two-level table, the raw lo / hi entries of
+// each level's base w_N^{i 2^t} at w[2 tl], w[2 tl + 1].  Issued right after
+// the leaf loads, all levels' lookups are ONE round trip beside them; looked
+// up inside tree_levels, each level's loads waited behind the previous level's
+// arithmetic (the compiler does not hoist them: a dependent load round trip
+// per level -- 3 of them at P = 8, ~2.9 us of config 2's 4.9-us load phase,
+// profiles/r06b_wg_clock_*).  Same values, same operations: bitwise equal.
+template <typename T, int L>
+struct TreeTwRegs {
+    cx<T> w[(1 << L) > 2 * L ? (1 << L) : 2 * L];
+};
+template <typename T, int L>
+__device__ __forceinline__ void tree_tw_fetch(TreeTwRegs<T, L>& r, const TreeTw& tw, uint64_t i, uint32_t log_d,
+                                              uint32_t t0) {
+    constexpr int V = 1 << L;
+    if (tw.direct) {
+#pragma unroll
+        for (int tl = 0; tl < L; tl++) {
+#pragma unroll
+            for (int ml = 0; ml < (V >> (tl + 1)); ml++)
+                r.w[V - (V >> tl) + ml] = tree_tw_lv<T>(tw, i + ((uint64_t)ml << log_d), t0 + (uint32_t)tl);
+        }
+    } else {
+        const cx<T>* lo = static_cast<const cx<T>*>(tw.lo);
+        const cx<T>* hi = static_cast<const cx<T>*>(tw.hi);
+#pragma unroll
+        for (int tl = 0; tl < L; tl++) {
+            const uint64_t E = i << (t0 + (uint32_t)tl);
+            r.w[2 * tl] = lo[E & ((1ull << tw.h) - 1)];
+            r.w[2 * tl + 1] = hi[E >> tw.h];
+        }
+    }
+}
+
 // Levels t0 .. t0+L-1 of the reference's radix-2 tree (CPU.c:419-448; level t
 // is the butterfly of size N >> t) on the 2^L values a thread holds at
 // positions base + i + m*2^log_d.  After the last of these levels v[m] lies
@@ -301,15 +338,19 @@ __device__ __forceinline__ cx<T> tree_tw_lv(const TreeTw& tw, uint64_t k, uint32
 // w_N^{i 2^t} * w_{2^(L-tl)}^{ml} (D 2^t / N = 2^(tl-L)): one table lookup
 // per level and thread, times a compile-time root (the fused pass's
 // tree_path_steps does the same), instead of one two-level lookup per
-// butterfly.
-template <typename T, int L>
+// butterfly.  PRE: the twiddles were fetched already (tree_tw_fetch, `pre`).
+template <typename T, int L, bool PRE = false>
 __device__ __forceinline__ void tree_levels(cx<T>* v, const TreeTw& tw, uint64_t i, uint32_t log_d, uint32_t t0,
-                                            uint64_t blk0, uint32_t log_w, uint64_t q0, uint64_t q1) {
+                                            uint64_t blk0, uint32_t log_w, uint64_t q0, uint64_t q1,
+                                            const TreeTwRegs<T, L>& pre = TreeTwRegs<T, L>{}) {
     constexpr int V = 1 << L;
     if (!tw.direct) {
         cx<T> base[L];
 #pragma unroll
-        for (int tl = 0; tl < L; tl++) base[tl] = tree_tw<T>(tw, i << (t0 + tl));
+        for (int tl = 0; tl < L; tl++) {
+            if constexpr (PRE) base[tl] = cmul(pre.w[2 * tl + 1], pre.w[2 * tl]);  // (= tw2)
+            else base[tl] = tree_tw<T>(tw, i << (t0 + tl));
+        }
         static_for<0, L, 1>([&](auto tlc) {
             constexpr int tl = decltype(tlc)::value;
             constexpr int BS = V >> tl, H = BS >> 1, NS = 1 << (L - tl);
@@ -350,7 +391,8 @@ __device__ __forceinline__ void tree_levels(cx<T>* v, const TreeTw& tw, uint64_t
                 const cx<T> x0 = v[lo + ml], x1 = v[lo + ml + H];
                 if (needL) v[lo + ml] = cadd(x0, x1);                      // butterfly_left
                 if (needR)  // butterfly_right: omega(N, b N/size), b = i + ml D
-                    v[lo + ml + H] = cmul(csub(x0, x1), tree_tw_lv<T>(tw, i + ((uint64_t)ml << log_d), t));
+                    v[lo + ml + H] = cmul(csub(x0, x1), PRE ? pre.w[V - (V >> tl) + ml]
+                                                            : tree_tw_lv<T>(tw, i + ((uint64_t)ml << log_d), t));
             }
         }
     }
@@ -468,11 +510,33 @@ struct PassArgs {
     // no scattered 16-B stores.
     uint32_t wil, wbrev;
 #ifdef PIFFT_WG_CLOCK
-    // diagnostics build only (tools/wg_clock.py): 3 words per workgroup --
-    // wall clock at entry, wall clock once its stores completed, hardware id
+    // diagnostics build only (tools/wg_clock.py): PIFFT_WGC_WORDS words per
+    // workgroup -- 0 wall clock at entry, 1 once its stores completed, 2 the
+    // hardware id, and thread 0's wall clock at each step of the chain: 3 the
+    // tile's inputs in registers (loads landed; MODE 11: the tree evaluated
+    // and handed to the first stage), 3 + S stage S's inputs received (S =
+    // 1 .. 3: after the exchange from stage S - 1), 7 the last stage's
+    // outputs computed (before the stores)
     unsigned long long* wg_clock;
 #endif
 };
+
+#ifdef PIFFT_WG_CLOCK
+#define PIFFT_WGC_WORDS 8
+// thread 0 stamps `slot` once its own outstanding loads / LDS reads have
+// landed (s_waitcnt 0); scheduling barriers keep the stamp in program order
+__device__ __forceinline__ void wgc_stamp(const PassArgs& a, int tid, int slot) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (a.wg_clock && tid == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        a.wg_clock[PIFFT_WGC_WORDS * blockIdx.x + slot] = wall_clock64();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+#define PIFFT_WGC(slot) wgc_stamp(a, tid, (slot))
+#else
+#define PIFFT_WGC(slot) ((void)0)
+#endif
 
 __device__ __forceinline__ uint64_t tile_of_block(uint32_t b, uint32_t log_xg, uint32_t nblocks) {
     if (log_xg == 0 || (nblocks & ((8u << log_xg) - 1))) return b;
@@ -723,6 +787,17 @@ constexpr int pre_count() {
     return pre_offset<R, C, BM, VPT, PassShape<R, VPT>::NSTG>();
 }
 
+// Workgroups per CU a k_pass instance is built for: two (PIFFT_MIN_WG_PER_CU),
+// one for the fused tree pass at P = 16 (its 16 leaves per input)
+// (config 3's single pass built for 8 waves per SIMD -- 64 VGPRs, 8 of its 16
+// workgroups per CU at once instead of 7 -- spills 18 B per lane and runs
+// 70 % slower: round 4, profiles/r04f_c3_wpe8.log)
+template <typename T, int R, int C, int MODE, int LP, int VPT>
+constexpr int pass_waves_per_eu() {
+    constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
+    return ((MODE & 3) == 3 && LP >= 5) ? 1 : ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
+}
+
 // MODE 11 = 3 | 8: the tree of ALL P = 2^LP workers fused into the first
 // worker-interleaved pass (an all-worker natural-order plan, PassArgs::wil =
 // LP).  The tile's C = J P launch lines are J adjacent line indices j times
@@ -798,11 +873,24 @@ __device__ __forceinline__ void wil_tree_to_lds(const PassArgs& a, T* lds, cx<T>
 #pragma unroll
         for (int m = 0; m < P; m++) w[u][m] = ld_stream<nt_loads(NTS)>(x + i + ((uint64_t)m << log_m));
     }
+    // every level's twiddles in one round trip beside the leaves (where the
+    // instance has the registers: <= 2 waves per SIMD, i.e. the latency-bound
+    // small tiles; the 128-VGPR streaming instances would spill)
+    constexpr bool PRE = pass_waves_per_eu<T, R, C, 11, LP, VPT>() <= 2;
+    TreeTwRegs<T, LP> trw[PRE ? PPT : 1];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int u = 0; u < PPT; u++) {
+            const int p = tid + u * NT;
+            tree_tw_fetch<T, LP>(trw[u], a.tree, j0 + (uint64_t)(p % J) + ((uint64_t)(p / J) << log_lb), log_m, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int u = 0; u < PPT; u++) {
         const int p = tid + u * NT;
         const uint64_t i = j0 + (uint64_t)(p % J) + ((uint64_t)(p / J) << log_lb);
-        tree_levels<T, LP>(w[u], a.tree, i, log_m, 0, 0, 0, 0, P);  // w[u][m] = z_m[i]
+        tree_levels<T, LP, PRE>(w[u], a.tree, i, log_m, 0, 0, 0, 0, P, trw[PRE ? u : 0]);  // w[u][m] = z_m[i]
     }
 #pragma unroll
     for (int comp = 0; comp < 2; comp++) {
@@ -865,6 +953,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     const uint32_t wil = WIL ? a.wil : 0u;
     const uint32_t lbi = log_lb + wil;
     const uint64_t lb_mask = (1ull << lbi) - 1;
+    if constexpr (S > 0 && S <= 3) PIFFT_WGC(3 + S);
 
     // MODE 2: the inter-pass twiddle factors depend only on (line, b); their
     // two-level table entries are fetched with the data, not after it (a
@@ -971,16 +1060,17 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             }
         }
     }
+    if constexpr (St::first) PIFFT_WGC(3);
     if constexpr (St::first && tw_prefetch<R, C, BM, VPT>()) {
         const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
         static_for<1, Sh::NSTG, 1>([&](auto sc) {
             constexpr int S2 = decltype(sc)::value;
-            using St2 = Stage<R, C, BM, S2, VPT>;
+            using St2 = Stage<R, C, SM, S2, VPT>;  // (the stage maps' mode: MODE 11 uses MODE 10's)
 #pragma unroll
             for (int u = 0; u < St2::U; u++) {
                 int c, b;
                 St2::map(tid, u, c, b);
-                pre[pre_offset<R, C, BM, VPT, S2>() + u] = twr[(b & (St2::ns - 1)) * (R / (St2::ns * St2::q))];
+                pre[pre_offset<R, C, SM, VPT, S2>() + u] = twr[(b & (St2::ns - 1)) * (R / (St2::ns * St2::q))];
             }
         });
     }
@@ -1017,7 +1107,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const int e1 = (b & (ns - 1)) * (R / (ns * q));
             C2 anc[4];
             if constexpr (tw_prefetch<R, C, BM, VPT>()) {
-                anc[0] = pre[pre_offset<R, C, BM, VPT, S>() + u];
+                anc[0] = pre[pre_offset<R, C, SM, VPT, S>() + u];
 #pragma unroll
                 for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
             } else {
@@ -1044,6 +1134,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     }
 
     if constexpr (St::last) {
+        PIFFT_WGC(7);
         // ---- outputs r' = b + k NB straight to HBM ----
         C2* __restrict__ out = static_cast<C2*>(a.out);
 #pragma unroll
@@ -1359,16 +1450,6 @@ constexpr int first_tw_count() {
     return (MODE & 3) == 2 ? 4 * Stage<R, C, 2, 0, VPT>::U : 1;
 }
 
-// Workgroups per CU a k_pass instance is built for: two (PIFFT_MIN_WG_PER_CU),
-// one for the fused tree pass at P = 16 (its 16 leaves per input)
-// (config 3's single pass built for 8 waves per SIMD -- 64 VGPRs, 8 of its 16
-// workgroups per CU at once instead of 7 -- spills 18 B per lane and runs
-// 70 % slower: round 4, profiles/r04f_c3_wpe8.log)
-template <typename T, int R, int C, int MODE, int LP, int VPT>
-constexpr int pass_waves_per_eu() {
-    constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
-    return ((MODE & 3) == 3 && LP >= 5) ? 1 : ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
-}
 
 // MODE 0: single pass (lines contiguous in and out, no inter-pass twiddle)
 // MODE 1: first pass of several (lines strided in, contiguous out, no twiddle)
@@ -1383,7 +1464,7 @@ void k_pass(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char pifft_smem[];
     constexpr int Q = PassShape<R, VPT>::Q;
     constexpr int TWN = first_tw_count<R, C, MODE, VPT>();
-    cx<T> pre[pre_count<R, C, MODE & 3, VPT>() > 0 ? pre_count<R, C, MODE & 3, VPT>() : 1];
+    cx<T> pre[pre_count<R, C, stage_mode(MODE), VPT>() > 0 ? pre_count<R, C, stage_mode(MODE), VPT>() : 1];
     // one tile per workgroup: a persistent tile loop (1, 2 or 4 resident
     // workgroups per CU walking the tiles) measured 1.4-1.7x slower at 2^28
     // fp64
@@ -1391,7 +1472,7 @@ void k_pass(PassArgs a) {
     T* lds = reinterpret_cast<T*>(pifft_smem);
     const int tid = (int)threadIdx.x;
 #ifdef PIFFT_WG_CLOCK
-    if (a.wg_clock && tid == 0) a.wg_clock[3 * blockIdx.x] = wall_clock64();
+    if (a.wg_clock && tid == 0) a.wg_clock[PIFFT_WGC_WORDS * blockIdx.x] = wall_clock64();
 #endif
     if constexpr (VPT == 32 && std::is_same_v<T, float> && PIFFT_PACK32) {
         cx<f2> vp[PassShape<R, VPT>::Q / 2];
@@ -1417,8 +1498,8 @@ void k_pass(PassArgs a) {
         __builtin_amdgcn_s_waitcnt(0);  // this thread's stores are done
         __syncthreads();
         if (tid == 0) {
-            a.wg_clock[3 * blockIdx.x + 1] = wall_clock64();
-            a.wg_clock[3 * blockIdx.x + 2] = __smid();
+            a.wg_clock[PIFFT_WGC_WORDS * blockIdx.x + 1] = wall_clock64();
+            a.wg_clock[PIFFT_WGC_WORDS * blockIdx.x + 2] = __smid();
         }
     }
 #endif

@@ -99,6 +99,12 @@ _SIGS = {
                                          ctypes.POINTER(ctypes.c_float)]),
     "pifft_allgather": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_P),
                                        ctypes.POINTER(ctypes.c_double)]),
+    "pifft_instance_count": (ctypes.c_int, []),
+    "pifft_instance_desc": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]),
+    "pifft_instance_found": (ctypes.c_int, [ctypes.c_int]),
+    "pifft_plan_dry_run_instances": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.POINTER(ctypes.c_int32), ctypes.c_int]),
 }
 SYMBOLS = tuple(_SIGS)
 
@@ -278,6 +284,42 @@ def describe_info(i: PlanInfo) -> dict:
         "vpt": list(i.vpt[: i.num_passes]),
         "worker_interleaved": bool(i.layout & 1), "natural_store": bool(i.layout & 2),
     }
+
+
+INSTANCE_FIELDS = ("prec", "R", "C", "mode", "nts", "lp", "vpt")
+
+
+def instances() -> list:
+    """Every compiled k_pass instance as (prec, R, C, MODE, NTS, LP, VPT), in
+    registry order (pifft_instance_desc)."""
+    out = []
+    d = (ctypes.c_int32 * 7)()
+    for i in range(lib().pifft_instance_count()):
+        _check(lib().pifft_instance_desc(i, d), "pifft_instance_desc")
+        out.append(tuple(d))
+    return out
+
+
+def instances_found() -> list:
+    """Registry indices of the instances the planner has found in this
+    process (pifft_instance_found): every instance a plan built so far
+    depends on."""
+    return [i for i in range(lib().pifft_instance_count()) if lib().pifft_instance_found(i) == 1]
+
+
+def dry_run_instances(n: int, workers: int = 1, batch: int = 1, prec: int = F64, *, first: int = 0,
+                      count: int | None = None, flags: int | None = None) -> list:
+    """The registry index of each launch's k_pass instance (-1: a tree or
+    interleave launch) of the plan pifft_plan_dry_run describes (flags as
+    dry_run: natural order for all workers, else slice-major)."""
+    count = workers if count is None else count
+    if flags is None:
+        flags = OUT_NATURAL if count == workers else OUT_SLICES
+    ids = (ctypes.c_int32 * MAX_LAUNCH_INFO)()
+    nl = lib().pifft_plan_dry_run_instances(n, workers, first, count, batch, prec, flags, ids, MAX_LAUNCH_INFO)
+    if nl < 0:
+        raise PifftError(f"pifft_plan_dry_run_instances: {last_error()}")
+    return list(ids[:min(nl, MAX_LAUNCH_INFO)])
 
 
 def dry_run(n: int, workers: int = 1, batch: int = 1, prec: int = F64, *, first: int = 0,

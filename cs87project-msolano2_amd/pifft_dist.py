@@ -149,9 +149,12 @@ def sample_bins(n: int, workers: int, per_worker: int = 8) -> list[int]:
 
 
 def max_over_ranks(value: float, device=None) -> float:
+    """The job's time: the largest value over the ranks (one all-reduce, on
+    `device` -- the GPU under RCCL, the CPU under gloo).  A world-size-1 group
+    runs the collective too (bench.py --pg: the RCCL path executed on one GPU)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -113,7 +113,8 @@ typedef struct pifft_plan_info {
                                   worker-interleaved; other bits reserved, never set);
                                   0 for tree and interleave launches */
     int32_t layout;          /* bit 0: worker-interleaved passes (all P <= 16 workers of a
-                                natural-order plan: the last pass writes natural order);
+                                natural-order plan -- P = 32 too for the one-launch plans
+                                of P N/P <= 8192 values: the last pass writes natural order);
                                 bit 1: the last pass stores natural order from the
                                 slice-major layout (small outputs); neither: slice-major
                                 passes (+ an interleave launch for natural order)   */
@@ -149,6 +150,23 @@ int pifft_plan_dry_run(uint64_t n, uint32_t workers, uint32_t first, uint32_t co
                        int prec, int flags, pifft_plan_info* info);
 
 int pifft_plan_get_info(const pifft_plan* plan, pifft_plan_info* info);
+
+/* Diagnostics (no reference counterpart): the registry of compiled k_pass
+ * instances, and which of them a plan would launch.  pifft_instance_desc
+ * writes {prec, R, C, MODE, NTS, LP, VPT} of instance i (< pifft_instance_count())
+ * to desc[0..6].  pifft_plan_dry_run_instances plans as pifft_plan_dry_run does
+ * and writes, for each launch i < min(launches, max_ids), the instance index of
+ * its k_pass kernel (-1 for tree and interleave launches); it returns the
+ * number of launches, or -1.  pifft_instance_found(i) is 1 once the planner
+ * has found instance i in this process (it probes instances to choose between
+ * plans, so a plan depends on every instance it found, launched or not), 0 if
+ * not, -1 for an index out of range.  tests/test_instances.py checks with
+ * them that every compiled instance is one some plan depends on. */
+int pifft_instance_count(void);
+int pifft_instance_desc(int i, int32_t* desc);
+int pifft_instance_found(int i);
+int pifft_plan_dry_run_instances(uint64_t n, uint32_t workers, uint32_t first, uint32_t count, uint32_t batch,
+                                 int prec, int flags, int32_t* ids, int max_ids);
 
 /* The kernel function of launch `launch` (< info.num_launches), demangled as
  * profilers print it (e.g. "void pifft::k_pass<double, 512, 16, 2, 1, 0, 16>

@@ -29,7 +29,7 @@ def _bench(*args, env_extra=None, tmp=None):
                        capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    multi = "--gpus" in args and args[args.index("--gpus") + 1] != "1"
+    multi = ("--gpus" in args and args[args.index("--gpus") + 1] != "1") or "--pg" in args
     assert len(lines) == (2 if multi else 1), r.stdout
     for ln in lines:
         assert len(ln) <= LINE_MAX_CHARS, len(ln)
@@ -199,3 +199,76 @@ def test_bench_exchange_failure_keeps_the_line():
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert "injected" in line["config"]["allgather_error"] and line["config"]["allgather_ms"] is None
     assert line["config"].get("verify") is None
+
+
+def test_bench_rccl_world_size_one():
+    """The multi-GPU code path under RCCL, executed on one GPU (round-5 verdict:
+    the driver's first 8-GPU run must not be its first execution): bench.py
+    --pg opens a 1-rank nccl group through torchrun -- init_process_group with
+    device_id, barrier(device_ids), the device-tensor all-reduce of
+    max_over_ranks, all_gather_object, all_gather_into_tensor of the complex
+    result, the self-check -- and configs 2 (8 workers on the one GPU) and 3
+    (the 4096 transforms on one rank) as multi_secondary runs them."""
+    d = _bench("--pg", "--dist-backend", "nccl", "--log-n", "20", "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline")
+    _common(d, 3, 1, n_gpus=1)
+    cfg = d["config"]
+    assert "per_rank_error" not in cfg and "allgather_error" not in cfg and "verify_error" not in cfg, cfg
+    assert [r["rank"] for r in cfg["per_rank"]] == [0] and cfg["per_rank"][0]["gpu"] == 0
+    assert cfg["allgather_ms"] > 0
+    v = cfg["verify"]
+    assert v["ok"] and v["slices_bitwise"] and v["slices_checked"] == 1 and v["rel_l2"] == 0.0 and v["bins_ok"], v
+    sec = cfg["secondary"]
+    assert set(sec) == {"C2_split", "C3_batch"}
+    for key, rec in sec.items():
+        assert "error" not in rec and "allgather_error" not in rec, (key, rec)
+        assert rec["value"] > 0 and rec["n_gpus"] == 1
+        _roofline_ok(rec["roofline_rank0"])
+    assert sec["C3_batch"]["batch_per_gpu"] == 4096
+    assert sec["C2_split"]["allgather_ms"] > 0 and sec["C2_split"]["verify"]["ok"], sec["C2_split"]
+    assert "8 workers" in sec["C2_split"]["workload"]
+
+
+_NCCL_ONE_RANK = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.path.join(sys.argv[1], "cs87project-msolano2_amd"))
+import pifft_dist
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+try:
+    assert dist.get_backend() == "nccl"
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for dt in (torch.complex128, torch.complex64):
+        x = torch.randn(3 * 4096, dtype=dt, generator=g).to(dev).view(3, 4096)
+        y = pifft_dist.allgather_slices(x)
+        assert y.is_cuda and y.dtype == dt and tuple(y.shape) == (3, 4096), (y.dtype, y.shape)
+        assert torch.equal(torch.view_as_real(y).view(torch.int32), torch.view_as_real(x).view(torch.int32))
+        assert pifft_dist.tensor_digest(y) == pifft_dist.tensor_digest(x)
+    r = pifft_dist.allgather_slices(torch.arange(10, dtype=torch.float64, device=dev))
+    assert torch.equal(r.cpu(), torch.arange(10, dtype=torch.float64))
+    assert pifft_dist.max_over_ranks(1.25, dev) == 1.25
+    rows = [None]
+    dist.all_gather_object(rows, {"rank": 0, "ms": 1.5})
+    assert rows == [{"rank": 0, "ms": 1.5}]
+    dist.barrier(device_ids=[0])
+    print("NCCL-ONE-RANK-OK", flush=True)
+finally:
+    dist.destroy_process_group()
+"""
+
+
+def test_pifft_dist_under_a_one_rank_rccl_group():
+    """pifft_dist's collectives on device tensors under RCCL (a 1-rank nccl
+    group on one GPU, in a child process): allgather_slices' complex view
+    through all_gather_into_tensor returns the input's bytes (complex128 and
+    complex64), max_over_ranks all-reduces a device tensor, all_gather_object
+    and barrier(device_ids) complete."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-c", _NCCL_ONE_RANK, ROOT], capture_output=True, text=True, timeout=180,
+                       env=env)
+    assert r.returncode == 0 and "NCCL-ONE-RANK-OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

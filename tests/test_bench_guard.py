@@ -106,6 +106,8 @@ def test_line_fits_the_driver_tail_with_every_config(world, tmp_path, capsys):
         assert k in line
     rf = line["roofline"]
     assert rf["frac"] == 0.6478 and rf["traffic"] and rf["kernel_name"] == KNAME and rf["checks"]["tol"] == 0.03
+    # the counters name their source: the committed PMC summary, not this run
+    assert rf["traffic_source"].startswith("profiles/") and "traffic" in rf["traffic_source"]
     assert line["cpu_baseline"]["value"] == 12.29 and line["cpu_baseline"]["cores"] == 16
     assert line["cpu_baseline"]["alternative"]["cores"] == 32
     sec = line["config"]["secondary"]
@@ -114,6 +116,7 @@ def test_line_fits_the_driver_tail_with_every_config(world, tmp_path, capsys):
     for rec in sec.values():
         r = rec.get("roofline") or rec.get("roofline_rank0")
         assert rec["value"] and rec["ms_per_step"] and r["frac"] and r["traffic"] and r["mean_ms"]
+        assert r["traffic_source"].startswith("profiles/")
         if world == 1:
             assert rec["cpu_baseline"]["value"] and rec["cpu_baseline"]["cores"] and rec["cpu_baseline"]["ms"]
     if world > 1:
@@ -140,6 +143,7 @@ def _guard_rank(rank, world, port, fault, q):
     os.environ["MASTER_PORT"] = str(port)
     if fault:
         os.environ["BENCH_FAULT"] = fault
+        os.environ["PIFFT_TUNING"] = "1"  # (BENCH_FAULT is read only under it)
     sys.path.insert(0, ROOT)
     import bench as b
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -215,3 +219,14 @@ def test_exchange_failure_keeps_the_line(fault):
         assert rec0["allgather_ms"] == 1.5 and "verify" not in rec0
     else:
         assert "allgather_ms" not in rec0 and "verify" not in rec0
+
+
+def test_bench_fault_needs_the_tuning_switch(monkeypatch):
+    """BENCH_FAULT is a test-only switch: without PIFFT_TUNING=1 a stray one in
+    the driver's environment injects nothing."""
+    monkeypatch.setenv("BENCH_FAULT", "allgather:0")
+    monkeypatch.delenv("PIFFT_TUNING")
+    bench._fault("allgather", 0)  # no exception
+    monkeypatch.setenv("PIFFT_TUNING", "1")
+    with pytest.raises(RuntimeError, match="injected"):
+        bench._fault("allgather", 0)

@@ -1009,14 +1009,16 @@ def test_allgather_errors():
         pifft.allgather(plans[:3] + [other], [b.data_ptr() for b in bufs], [nat.data_ptr(), None, None, None])
 
 
-@pytest.mark.parametrize("site", ["enable_peer", "broadcast", "peer_copy"])
+@pytest.mark.parametrize("site", ["enable_peer", "broadcast", "peer_copy", "peer_copy:3"])
 def test_multi_gpu_error_paths_fail_cleanly(site, monkeypatch):
     """The multi-GPU error branches (peer access, the xGMI input broadcast of
     pifft_execute_group, the peer copies of pifft_allgather), reached on one
     GPU through the test-only fault switch (PIFFT_TUNING=1 PIFFT_FAULT=<site>):
     each call returns -1 with the message (CPU.c:102-109's -1 + message), holds
     no more device memory afterwards than before, and the next call on the
-    same plans succeeds with the same bytes."""
+    same plans succeeds with the same bytes.  peer_copy:3 fails the third copy
+    of the all-gather, after two copies were enqueued: the part-way cleanup
+    (waiting for the copies in flight before returning) runs."""
     n, P, batch = 1 << 16, 8, 2
     x = oracle.generate(n * batch, np.complex128, seed=31)
     plans = [pifft.Plan(n, P, batch, pifft.F64, first=q, count=1, device=0) for q in range(P)]
@@ -1036,7 +1038,7 @@ def test_multi_gpu_error_paths_fail_cleanly(site, monkeypatch):
     monkeypatch.setenv("PIFFT_FAULT", site)
     got = np.zeros(n * batch, np.complex128)
     with pytest.raises(pifft.PifftError, match="injected fault"):
-        if site == "peer_copy":
+        if site.startswith("peer_copy"):
             pifft.allgather(plans, [sl.data_ptr() for sl in slices], [nat.data_ptr()] + [None] * (P - 1))
         else:
             pifft.execute_group(plans, x, got)

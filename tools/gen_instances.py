@@ -107,9 +107,12 @@ for R in (256, 512):
             items.append(f"PKV(double, 64, {R}, {C}, 2, {nts}, 0, 8),")
 # MODE 11 = 3 | 8: the tree of all P workers fused into the first
 # worker-interleaved pass (round 5).  A tile is J adjacent line indices x the P
-# workers (C = J P lines) at the 8192-value tile (R = 8192 / C): J = 16 fp64 /
-# 32 fp32 (256-B leaf rows, the planner's default) and half that
-# (PIFFT_WIL_FUSE_J, tuning), P = 2..16.
+# workers (C = J P lines) at the 8192-value tile (R = 8192 / C), P = 2..16.
+# The planner's J (build_plan, pifft.hip): fp64 J = 8 (P <= 8, and P = 16 from
+# 256 MiB); fp32 J = 8 up to 32 MiB and 16 up to 1 GiB; J = 4 (4096-value tile
+# below 256 workgroups, or where J = 8 would split the remainder) and J = 2
+# (fp64 P = 16, 32-64 MiB) as refinements below; other J only under
+# PIFFT_WIL_FUSE_J (tuning).  Candidates: fp64 J = 16/8/4, fp32 J = 32/16/8.
 for T, prec, js in (("double", 64, (16, 8, 4)), ("float", 32, (32, 16, 8))):
     for J in js:
         for lp in (1, 2, 3, 4):
@@ -163,7 +166,40 @@ for T, prec, ms in (("double", 64, (32, 64, 128)), ("float", 32, (32, 64, 128, 2
 # (8 values per thread -- PKV(..., 8), radix-8 stages -- measured slower than
 # 16 for every single pass and batch tried, fp32 4096 x 128..4096 and fp64
 # 2^12 / 2^13 x 1..1024 (profiles/r02_vpt_sweep.log): not instantiated)
-d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cs87project-msolano2_amd", "csrc")
+# Round 6: only the instances some plan launches are compiled.  The rules
+# above are the candidates; the kept ones are those the default planner
+# launches over its whole domain (tools/instance_sweep.py ->
+# tests/golden/instances_default.txt) and those the GPU tests' plans launch
+# under their tuning variables (conftest.py's PIFFTTEST_RECORD_INSTANCES ->
+# tests/golden/instances_tests.txt).  A tuning variable that asks for a
+# dropped instance gets the planner's "no pass kernel" error.
+# tests/test_instances.py checks both lists against the built library.
+# `--all`: every candidate (to re-derive the lists after a planner change).
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def desc(item: str) -> str:
+    m = re.match(r"PK(V?)\((\w+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)(?:, (\d+))?\),", item)
+    prec, R, C, mode, nts, lp = (int(m.group(k)) for k in range(3, 9))
+    vpt = int(m.group(9)) if m.group(1) else 16
+    return "prec=%d R=%d C=%d mode=%d nts=%d lp=%d vpt=%d" % (prec, R, C, mode, nts, lp, vpt)
+
+
+keep = set()
+for name in ("instances_default.txt", "instances_tests.txt"):
+    path = os.path.join(ROOT, "tests", "golden", name)
+    if os.path.exists(path):
+        keep |= {ln.strip() for ln in open(path) if ln.strip()}
+candidates = len(items)
+if keep and "--all" not in sys.argv:
+    items = [it for it in items if desc(it) in keep]
+    missing = keep - {desc(it) for it in items}
+    assert not missing, f"kept instances no rule generates: {sorted(missing)[:5]}"
+print(f"{candidates} candidate instances, {len(items)} kept")
+d = os.path.join(ROOT, "cs87project-msolano2_amd", "csrc")
 for k in range(NPART):
     with open(os.path.join(d, f"pifft_instances_{k}.inc"), "w") as f:
         f.write(f"// generated by tools/gen_instances.py -- part {k} of {NPART}\n")

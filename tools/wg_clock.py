@@ -4,12 +4,18 @@
 Needs the diagnostics build (EXTRA=-DPIFFT_WG_CLOCK tools/mkvariant.sh
 wgclock -> abvar/wgclock.so): every workgroup of the clocked launch records
 its entry wall clock (100 MHz), the wall clock once its stores completed and
-its hardware id.  Per pass launch of the plan this prints the kernel's
-event-bound duration beside the workgroups' timeline:
+its hardware id, and thread 0 stamps each step of the load -> exchanges ->
+store chain (PassArgs::wg_clock, 8 words per workgroup).  Per pass launch of
+the plan this prints the kernel's event-bound duration beside the
+workgroups' timeline:
   ramp   -- last workgroup entry - first entry (dispatch of the grid),
   wg     -- one workgroup's entry to stores-done (min / median / max),
   span   -- first entry to last stores-done,
-so duration - span is the launch's fixed cost outside the workgroups.
+so duration - span is the launch's fixed cost outside the workgroups; and the
+median workgroup's chain, step by step (us): load (entry -> inputs in
+registers; MODE 11: -> the tree's values handed to the first stage), s1..s3
+(stage S-1's butterflies + the exchange into stage S), last (the last stage's
+butterflies), store (-> stores completed).
 
 usage: PIFFT_LIB=abvar/wgclock.so python3 tools/wg_clock.py --log-n 20 [--workers 8 --count 1] [--prec 64]
 """
@@ -64,7 +70,9 @@ def main():
         dump.write("launch,rep,wg,start_us,end_us,hw_id\n")
     for li in range(d["num_launches"]):
         name = plan.kernel_name(li)
-        buf = (ctypes.c_ulonglong * (3 * 65536))()
+        W = 8  # PIFFT_WGC_WORDS
+        buf = (ctypes.c_ulonglong * (W * 65536))()
+        steps = []
         hz = ctypes.c_ulonglong()
         rows = []
         for _ in range(args.reps):
@@ -74,15 +82,25 @@ def main():
                 print(f"launch {li} ({name}): {pifft.last_error()}")
                 break
             us = 1e6 / hz.value
-            t0 = [buf[3 * w] for w in range(nwg)]
-            t1 = [buf[3 * w + 1] for w in range(nwg)]
+            t0 = [buf[W * w] for w in range(nwg)]
+            t1 = [buf[W * w + 1] for w in range(nwg)]
+            for w in range(nwg):  # the chain: entry, inputs, stages 1..3 reached, last computed, stores done
+                marks = [buf[W * w]] + [buf[W * w + k] for k in (3, 4, 5, 6, 7)] + [buf[W * w + 1]]
+                row, prev = [], marks[0]
+                for m in marks[1:]:
+                    if m == 0:  # (a stage this pass does not have)
+                        row.append(None)
+                        continue
+                    row.append((m - prev) * us)
+                    prev = m
+                steps.append(row)
             durs = sorted((b - a) * us for a, b in zip(t0, t1))
             if dump:
                 m0 = min(t0)
                 for w in range(nwg):
-                    dump.write(f"{li},{len(rows)},{w},{(t0[w] - m0) * us:.2f},{(t1[w] - m0) * us:.2f},{buf[3 * w + 2]}\n")
+                    dump.write(f"{li},{len(rows)},{w},{(t0[w] - m0) * us:.2f},{(t1[w] - m0) * us:.2f},{buf[W * w + 2]}\n")
             rows.append(((max(t0) - min(t0)) * us, durs[0], statistics.median(durs), durs[-1],
-                         (max(t1) - min(t0)) * us, len({buf[3 * w + 2] for w in range(nwg)})))
+                         (max(t1) - min(t0)) * us, len({buf[W * w + 2] for w in range(nwg)})))
         if not rows:
             continue
         med = [statistics.median(r[k] for r in rows) for k in range(6)]
@@ -90,6 +108,13 @@ def main():
         print(f"  launch {li} {d['launch_kind'][li]:9s} {nwg:5d} WGs  event {dur:7.2f} us | ramp {med[0]:6.2f} | "
               f"wg {med[1]:6.2f} / {med[2]:6.2f} / {med[3]:6.2f} | span {med[4]:6.2f} | outside {dur - med[4]:6.2f} us"
               f"  ({int(med[5])} hw ids)  {name}")
+        names = ("load", "s1", "s2", "s3", "last", "store")
+        parts = []
+        for k, nm in enumerate(names):
+            vals = [r[k] for r in steps if r[k] is not None]
+            if vals:
+                parts.append(f"{nm} {statistics.median(vals):5.2f}")
+        print("      chain (median workgroup, us): " + " | ".join(parts))
 
 
 if __name__ == "__main__":
