@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """tools/check_rooflines.py <bench.json> <rocpd2summary dir> <rocpd .db> [--same-run] --
 checks every roofline of a bench line against rocprofv3 --kernel-trace of the
-same bench command in the same session (tools/gpu_r04.sh).
+same bench command in the same session (tools/gpu_session.sh, stage s).
 
 The traced run executes the configs in bench.py's order (headline, then the
 secondary configs).  Dispatches are split into one cluster per config at each

@@ -1,5 +1,5 @@
 #!/bin/bash
-# tools/gpu_r05.sh <tag> <stages> [tests...] -- one GPU session of round-5 evidence.
+# tools/gpu_session.sh <tag> <stages> [tests...] -- one GPU evidence session (rounds 5-6).
 # stages: any of t (GPU tests + smoke), b (bench.py as the driver runs it; the
 #   printed line, and its sidecar with the per-launch detail),
 #   s (rocprofv3 --kernel-trace --stats of bench.py in the same session, then
