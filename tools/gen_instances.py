@@ -133,7 +133,10 @@ for nts in (0, 1):
     items.append(f"PK(float, 32, 256, 32, 11, {nts}, 3),")
     items.append(f"PK(float, 32, 128, 64, 11, {nts}, 4),")    # fp32 P = 16, J = 4
     items.append(f"PK(double, 64, 256, 32, 11, {nts}, 4),")   # fp64 P = 16, J = 2
-    items.append(f"PK(double, 64, 256, 16, 11, {nts}, 3),")   # fp64 P = 8, J = 2 (round 6 A/B: config 2 on 256 CUs twice)
+# (fp64 P = 8 at J = 2 / 4096-value tile -- radices 256.512, both passes on
+# 256 CUs instead of 128.1024, whose second pass has 128 workgroups: config 2
+# 22.2 -> 22.9 us, 2^21 P = 8 33 -> 39 us, 2^19 +1 %; round 6,
+# profiles/r06e_c2_j2.txt; not instantiated)
 # ... and the one-launch form: a transform of P M <= 8192 values (from 1024)
 # as ONE fused pass at J = 1 -- C = P lines of R = M points, every worker's
 # tree then its whole M-point FFT, natural-order store (round 5; the

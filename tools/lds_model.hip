@@ -142,7 +142,7 @@ static void list(std::vector<Instr>& v) {
     exchanges<T, R, C, MODE, 0, VPT>(v);
 }
 
-#define I(T, R, C, M) Inst{#T, (int)sizeof(T), R, C, M, 16, &list<T, R, C, M, 16>}
+#define I(T, R, C, M, V) Inst{#T, (int)sizeof(T), R, C, M, V, &list<T, R, C, M, V>}
 // every (precision, R, C, mode) with an LDS exchange that the instance tables hold
 static std::vector<Inst> instances() {
     std::vector<Inst> v;
@@ -226,8 +226,8 @@ int main(int argc, char** argv) {
         const Cost c0 = evaluate(ins, lds_default_of(in.R), in.esz);
         Cost cb;
         const LdsLayout b = search(in, ins, cb);
-        printf("%-6s R=%5d C=%2d mode=%d  default %.3f (%ld+%ld)  best %.3f (%ld+%ld) ls=%d xs=%d xm=%d ps=%d cm=%d cs=%d\n",
-               in.tname, in.R, in.C, in.mode, c0.ratio(), c0.base, c0.extra, cb.ratio(), cb.base, cb.extra, b.ls, b.xs,
+        printf("%-6s R=%5d C=%2d mode=%d vpt=%2d  default %.3f (%ld+%ld)  best %.3f (%ld+%ld) ls=%d xs=%d xm=%d ps=%d cm=%d cs=%d\n",
+               in.tname, in.R, in.C, in.mode, in.vpt, c0.ratio(), c0.base, c0.extra, cb.ratio(), cb.base, cb.extra, b.ls, b.xs,
                b.xm, b.ps, b.cm, b.cs);
         fflush(stdout);
         if (out && cb.base + cb.extra < c0.base + c0.extra)
