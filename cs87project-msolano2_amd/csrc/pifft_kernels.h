@@ -1241,6 +1241,21 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 // 174 VGPRs in MODE 2 and spills at 128).  Loads, stores and LDS exchanges
 // address each half with the VPT-32 Stage map of its own butterfly.
 // ---------------------------------------------------------------------------
+// Diagnostics builds only (timing, WRONG results; never the product): the
+// packed fp32 passes without their twiddles (PIFFT_DIAG_NO_TW=1: no table
+// loads, no twiddle products) or without their butterflies
+// (PIFFT_DIAG_NO_DFT=1), to split a pass's time between its data movement,
+// LDS exchanges, twiddles and arithmetic (round 6, tools/gpu_r06g.sh).
+#ifndef PIFFT_DIAG_NO_TW
+#define PIFFT_DIAG_NO_TW 0
+#endif
+#ifndef PIFFT_DIAG_NO_DFT
+#define PIFFT_DIAG_NO_DFT 0
+#endif
+template <int q, typename V>
+__device__ __forceinline__ void dft_diag(V* v) {
+    if constexpr (!PIFFT_DIAG_NO_DFT) dft<q>(v);
+}
 #ifndef PIFFT_PK_REMAT
 #define PIFFT_PK_REMAT 1  // packed VPT-32 exchanges: LDS addresses recomputed per component
 #endif
@@ -1287,7 +1302,7 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
     constexpr bool share_anc = St::cfast && U > 1 && St::NT % C == 0;
 
     if constexpr (St::first) {
-        if constexpr (BM == 2) {
+        if constexpr (BM == 2 && !PIFFT_DIAG_NO_TW) {
             const C1* tlo = static_cast<const C1*>(a.tw_lo);
             const C1* thi = static_cast<const C1*>(a.tw_hi);
             const uint64_t hmask = (1ull << a.tw_h) - 1;
@@ -1329,7 +1344,7 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
         });
     }
     // ---- twiddles and butterflies, one packed pair of butterflies at a time ----
-    if constexpr (St::first && BM == 2) {
+    if constexpr (St::first && BM == 2 && !PIFFT_DIAG_NO_TW) {
         C1 anc0[4], anc1[4];
         if constexpr (share_anc) {
             anc0[0] = cmul(twp[1], twp[0]);
@@ -1351,13 +1366,13 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
 #pragma unroll
             for (int i = 0; (1 << i) < q; i++) ap[i] = pk_pair(anc0[i], share_anc ? anc0[i] : anc1[i]);
             apply_powers<q>(&vp[m * q], ap);
-            dft<q>(&vp[m * q]);
+            dft_diag<q>(&vp[m * q]);
             const CP base = pk_pair(cmul(twp[4 * (2 * m) + 3], twp[4 * (2 * m) + 2]),
                                     cmul(twp[4 * (2 * m + 1) + 3], twp[4 * (2 * m + 1) + 2]));
 #pragma unroll
             for (int k = 0; k < q; k++) vp[m * q + k] = cmul(vp[m * q + k], base);
         }
-    } else if constexpr (!St::first) {
+    } else if constexpr (!St::first && !PIFFT_DIAG_NO_TW) {
         // w_{ns q}^{(b mod ns) k} = w_R^{(b mod ns) k R/(ns q)}, per butterfly
         const C1* __restrict__ twr = static_cast<const C1*>(a.tw_r);
 #pragma unroll
@@ -1370,11 +1385,11 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
 #pragma unroll
             for (int i = 0; (1 << i) < q; i++) ap[i] = pk_pair(twr[e0 << i], twr[e1 << i]);
             apply_powers<q>(&vp[m * q], ap);
-            dft<q>(&vp[m * q]);
+            dft_diag<q>(&vp[m * q]);
         }
     } else {
 #pragma unroll
-        for (int m = 0; m < U / 2; m++) dft<q>(&vp[m * q]);
+        for (int m = 0; m < U / 2; m++) dft_diag<q>(&vp[m * q]);
     }
 
     if constexpr (St::last) {

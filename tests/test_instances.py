@@ -8,10 +8,11 @@ verdict: 1474 instances, 6.3 MB, several of them reachable by no plan).
     tests/golden/instances_default.txt -- a planner change that reaches a new
     instance, or stops using one, shows here;
   * every compiled instance is in that list or in
-    tests/golden/instances_tests.txt, the instances the GPU tests' plans
-    launch under their tuning variables (recorded on MI355X with
-    PIFFTTEST_RECORD_INSTANCES, conftest.py) -- nothing is compiled that no
-    plan launches.
+    tests/golden/instances_tests.txt / instances_tests_cpu.txt, the instances
+    the GPU tests' plans (recorded on MI355X) and the CPU tests' dry runs
+    depend on under their tuning variables (PIFFTTEST_RECORD_INSTANCES,
+    conftest.py) -- nothing is compiled that no plan depends on, and nothing
+    a plan depends on is left out.
 Host-side planning only (pifft_plan_dry_run_instances): no GPU."""
 import os
 import sys
@@ -76,7 +77,7 @@ def test_default_planner_uses_the_committed_list(default_used, registry):
 
 
 def test_every_compiled_instance_is_used(registry):
-    used = _read("instances_default.txt") | _read("instances_tests.txt")
+    used = _read("instances_default.txt") | _read("instances_tests.txt") | _read("instances_tests_cpu.txt")
     unused = registry - used
     assert not unused, f"{len(unused)} compiled instances no plan launches, e.g. {sorted(unused)[:5]}"
     dropped = used - registry

@@ -175,7 +175,8 @@ for T, prec, ms in (("double", 64, (32, 64, 128)), ("float", 32, (32, 64, 128, 2
 # launches over its whole domain (tools/instance_sweep.py ->
 # tests/golden/instances_default.txt) and those the GPU tests' plans launch
 # under their tuning variables (conftest.py's PIFFTTEST_RECORD_INSTANCES ->
-# tests/golden/instances_tests.txt).  A tuning variable that asks for a
+# tests/golden/instances_tests.txt from the GPU suite on MI355X,
+# instances_tests_cpu.txt from the CPU suite's tuned dry runs).  A tuning variable that asks for a
 # dropped instance gets the planner's "no pass kernel" error.
 # tests/test_instances.py checks both lists against the built library.
 # `--all`: every candidate (to re-derive the lists after a planner change).
@@ -193,7 +194,7 @@ def desc(item: str) -> str:
 
 
 keep = set()
-for name in ("instances_default.txt", "instances_tests.txt"):
+for name in ("instances_default.txt", "instances_tests.txt", "instances_tests_cpu.txt"):
     path = os.path.join(ROOT, "tests", "golden", name)
     if os.path.exists(path):
         keep |= {ln.strip() for ln in open(path) if ln.strip()}

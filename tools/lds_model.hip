@@ -230,7 +230,11 @@ int main(int argc, char** argv) {
                in.tname, in.R, in.C, in.mode, in.vpt, c0.ratio(), c0.base, c0.extra, cb.ratio(), cb.base, cb.extra, b.ls, b.xs,
                b.xm, b.ps, b.cm, b.cs);
         fflush(stdout);
-        if (out && cb.base + cb.extra < c0.base + c0.extra)
+        // (VPT 32, the packed fp32 passes: modelled since round 6 and reported,
+        // but their searched layouts -- fp32 last pass 43 -> 20 % conflict
+        // cycles -- ran no faster on MI355X (fp32 2^28 2.47 vs 2.49 ms,
+        // profiles/r06f_ab_fp32_2e28.txt): they keep the default layout)
+        if (out && in.vpt != 32 && cb.base + cb.extra < c0.base + c0.extra)
             fprintf(out, "template <> struct LdsPick<%s, %d, %d, %d, %d> { static constexpr LdsLayout value{%d, %d, %d, %d, %d, %d}; };\n",
                     in.tname, in.R, in.C, in.mode, in.vpt, b.ls, b.xs, b.xm, b.ps, b.cm, b.cs);
     }
