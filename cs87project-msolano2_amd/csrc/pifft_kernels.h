@@ -1256,6 +1256,9 @@ template <int q, typename V>
 __device__ __forceinline__ void dft_diag(V* v) {
     if constexpr (!PIFFT_DIAG_NO_DFT) dft<q>(v);
 }
+#ifndef PIFFT_PK_SERIAL
+#define PIFFT_PK_SERIAL 0  // packed passes: a scheduling barrier after each butterfly pair (tuning A/B)
+#endif
 #ifndef PIFFT_PK_REMAT
 #define PIFFT_PK_REMAT 1  // packed VPT-32 exchanges: LDS addresses recomputed per component
 #endif
@@ -1367,6 +1370,7 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
             for (int i = 0; (1 << i) < q; i++) ap[i] = pk_pair(anc0[i], share_anc ? anc0[i] : anc1[i]);
             apply_powers<q>(&vp[m * q], ap);
             dft_diag<q>(&vp[m * q]);
+            if constexpr (PIFFT_PK_SERIAL) __builtin_amdgcn_sched_barrier(0);
             const CP base = pk_pair(cmul(twp[4 * (2 * m) + 3], twp[4 * (2 * m) + 2]),
                                     cmul(twp[4 * (2 * m + 1) + 3], twp[4 * (2 * m + 1) + 2]));
 #pragma unroll
@@ -1386,10 +1390,14 @@ __device__ __forceinline__ void pass_stages_packed(const PassArgs& a, float* lds
             for (int i = 0; (1 << i) < q; i++) ap[i] = pk_pair(twr[e0 << i], twr[e1 << i]);
             apply_powers<q>(&vp[m * q], ap);
             dft_diag<q>(&vp[m * q]);
+            if constexpr (PIFFT_PK_SERIAL) __builtin_amdgcn_sched_barrier(0);
         }
     } else {
 #pragma unroll
-        for (int m = 0; m < U / 2; m++) dft_diag<q>(&vp[m * q]);
+        for (int m = 0; m < U / 2; m++) {
+            dft_diag<q>(&vp[m * q]);
+            if constexpr (PIFFT_PK_SERIAL) __builtin_amdgcn_sched_barrier(0);
+        }
     }
 
     if constexpr (St::last) {
