@@ -117,18 +117,28 @@ def _sweep_plans(log_n: int):
     return sweep_one(log_n, True)
 
 
-def sweep(jobs: int = 8, logs=range(1, 33), with_plans: bool = False):
-    """Every instance the default planner launches over the domain:
-    {index: (prec, R, C, MODE, NTS, LP, VPT)} plus one shape using each."""
-    import pifft
-    for k in list(os.environ):  # the default planner: no tuning variable
+def _default_planner_env():
+    """Worker-process initializer: the default planner, no tuning variable
+    (the caller's own environment is left as it is)."""
+    for k in list(os.environ):
         if k.startswith("PIFFT_") and k != "PIFFT_LIB":
             del os.environ[k]
+
+
+def sweep(jobs: int = 8, logs=range(1, 33), with_plans: bool = False):
+    """Every instance the default planner launches or finds over the domain:
+    ({index: one shape using it (None: found while choosing)}), with the
+    registry table and the count of shapes the ABI refuses."""
+    import multiprocessing
+    import pifft
     table = pifft.instances()
     used = {}
     errors = 0
     plans = {}
-    with ProcessPoolExecutor(max_workers=jobs) as ex:
+    # fresh worker processes (spawn): each starts with an empty found-log
+    # and the default planner's environment
+    ctx = multiprocessing.get_context("spawn")
+    with ProcessPoolExecutor(max_workers=jobs, mp_context=ctx, initializer=_default_planner_env) as ex:
         for got, err, by_shape in ex.map(_sweep_plans if with_plans else sweep_one, list(logs)):
             errors += err
             plans.update(by_shape)
