@@ -258,7 +258,8 @@ int pifft_execute(pifft_plan* plan, const void* host_in, void* host_out, double*
 /* Several plans (normally one per GPU) run concurrently from one host thread:
  * the P-GPU no-communication split.  Stage times are the max over plans.
  * When the plans hold all P workers between them (PIFFT_OUT_SLICES), host_out
- * is filled through pifft_allgather onto the first plan's device and one
+ * is filled through pifft_allgather onto the first plan's device (into a
+ * batch*N buffer allocated for the call and freed before it returns) and one
  * device-to-host copy; otherwise a plan whose output is natural order or the
  * reference's scratch order (PIFFT_OUT_BITREV) is copied straight into
  * host_out, and a plan holding only some workers has its bins scattered on
