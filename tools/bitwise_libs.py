@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""tools/bitwise_libs.py LIB -- run a list of plans through this process's
+libpifft (PIFFT_LIB) and write each output's SHA-256 to stdout; two runs with
+two builds, diffed, show whether a kernel change kept the results bit for bit
+(round 6: the one-round-trip tree twiddle fetch, tree_tw_fetch, against the
+round-5 kernels).  usage: PIFFT_LIB=abvar/x.so python3 tools/bitwise_libs.py"""
+import hashlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cs87project-msolano2_amd"))
+
+import torch  # noqa: E402  (before libpifft: one HIP runtime)
+import pifft  # noqa: E402
+
+SHAPES = [(20, 8, 1, 64), (19, 8, 1, 64), (20, 4, 1, 64), (18, 4, 1, 64), (22, 8, 1, 64), (20, 2, 1, 64),
+          (20, 8, 1, 32), (18, 8, 1, 32), (21, 8, 1, 32), (12, 8, 64, 64), (17, 8, 16, 64), (24, 8, 1, 64)]
+
+for logn, P, batch, prec in SHAPES:
+    n = 1 << logn
+    cdt = torch.complex128 if prec == 64 else torch.complex64
+    x = torch.empty(n * batch, dtype=cdt, device="cuda")
+    pifft.generate_device(x.data_ptr(), n * batch, n, prec, seed=logn * 7 + P)
+    plan = pifft.Plan(n, P, batch, prec)
+    y = torch.empty(plan.describe()["out_elems"], dtype=cdt, device="cuda")
+    plan.execute_device(x.data_ptr(), y.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    h = hashlib.sha256(y.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(f"n=2^{logn} P={P} batch={batch} f{prec} {plan.kernel_name(0)[:60]} {h}", flush=True)
+    plan.close()
