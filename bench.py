@@ -322,6 +322,17 @@ def headline_cpu_baseline(log_n: int, prec: int, batch: int = 1, threads: int | 
                 rec["alternative"] = {k: alt[k] for k in keep if k in alt}
         except Exception as e:  # reported, never silently replaced
             rec["alternative"] = {"value": None, "cores": p_ref, "error": repr(e)}
+    # the reference Makefile's own flags (-g, i.e. -O0, cpu/Makefile:21) beside
+    # the -O2 build, at the same p; fp64 (oracle/_ref's -O0 build)
+    if prec == 64 and batch == 1 and os.environ.get("BENCH_CPU_O0", "1") == "1":
+        try:
+            import pifft_oracle as oracle
+            exe0 = os.path.join(os.path.dirname(oracle.reference_binary(64)), "fourier-parallel-pi-cpu-pthreads-f64-O0")
+            ms0, wall0 = _run_ref(exe0, 1 << cl, rec["cores"])
+            rec["O0"] = {"value": round(5.0 * (1 << cl) * cl / (ms0 * 1e6), 4), "cores": rec["cores"],
+                         "ms": round(ms0, 3), "wall_s": round(wall0, 1)}
+        except Exception as e:  # reported, never silently replaced
+            rec["O0"] = {"value": None, "error": repr(e)[:200]}
     return rec
 
 
@@ -878,6 +889,8 @@ def _short_sample(cb: dict) -> dict:
     alt = cb.get("alternative") if cb else None
     if alt:
         out["alternative"] = _pick(alt, ("value", "cores", "ms", "error"))
+    if cb and cb.get("O0"):
+        out["O0"] = _pick(cb["O0"], ("value", "cores", "ms", "error"))
     return out
 
 

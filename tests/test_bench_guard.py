@@ -44,7 +44,8 @@ def _cpu():
             "host_bytes_touched": 107374182400, "child_peak_rss_GiB": 99.99, "cpu_model": "AMD EPYC 9575F",
             "host_cpus": 256, "physical_cores": 128, "cpu_affinity": 256, "cgroup_cpu_quota": 16.0,
             "mem_available_GiB": 2920.8, "cgroup_mem_limit_GiB": 300.1, "cpu_share": 16, "selection": "x" * 120,
-            "alternative": {"value": 7.1, "cores": 32, "ms": 5300.0, "sample": "y" * 300}}
+            "alternative": {"value": 7.1, "cores": 32, "ms": 5300.0, "sample": "y" * 300},
+            "O0": {"value": 5.3, "cores": 16, "ms": 7100.0, "wall_s": 40.2}}
 
 
 def _launches(nl):
@@ -110,6 +111,8 @@ def test_line_fits_the_driver_tail_with_every_config(world, tmp_path, capsys):
     assert rf["traffic_source"].startswith("profiles/") and "traffic" in rf["traffic_source"]
     assert line["cpu_baseline"]["value"] == 12.29 and line["cpu_baseline"]["cores"] == 16
     assert line["cpu_baseline"]["alternative"]["cores"] == 32
+    # the reference Makefile's own -O0 build beside the -O2 one
+    assert line["cpu_baseline"]["O0"] == {"value": 5.3, "cores": 16, "ms": 7100.0}
     sec = line["config"]["secondary"]
     want = {"C1", "C2", "C2_slice", "C3", "C4_f32"} if world == 1 else {"C2_split", "C3_batch", "C5"}
     assert set(sec) == want
