@@ -102,3 +102,13 @@ def test_headline_cpu_baseline_runs_the_reference():
               "child_peak_rss_GiB"):
         assert k in rec, k
     assert "p=2 pthreads" in rec["sample"]
+
+
+def test_pg_is_a_process_group_option():
+    """--pg opens a process group at one rank (bench.py's multi-GPU branch on
+    one GPU); it cannot be combined with --as-rank, the single-process
+    emulation of another rank's plan."""
+    r = _run(["--pg", "--as-rank", "0/2"], {})
+    assert r.returncode != 0 and "--as-rank" in r.stderr
+    r = _run(["--pg", "--as-rank", "0/2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "--as-rank" in r.stderr

@@ -239,3 +239,28 @@ def test_verify_finish_accepts_and_rejects():
     v = bench.verify_finish(torch, good, None)
     assert v["ok"] and v["rel_l2"] is None and "slices only" in v["note"]
     assert bench.verify_finish(torch, {}, X) is None  # ranks other than 0
+
+
+def test_one_rank_group_runs_the_collectives(monkeypatch):
+    """A world-size-1 group (bench.py --pg) executes pifft_dist's collectives
+    instead of short-cutting them: max_over_ranks all-reduces, and
+    allgather_slices returns the rank's own bytes (gloo here; the RCCL leg is
+    tests/test_bench.py::test_pifft_dist_under_a_one_rank_rccl_group)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "cs87project-msolano2_amd"))
+    import pifft_dist
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        calls = []
+        orig = dist.all_reduce
+        monkeypatch.setattr(dist, "all_reduce", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+        assert pifft_dist.max_over_ranks(1.25) == 1.25 and calls == [1]
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(2, 512, dtype=torch.complex128, generator=g)
+        y = pifft_dist.allgather_slices(x)
+        assert y.shape == x.shape and torch.equal(torch.view_as_real(y), torch.view_as_real(x))
+    finally:
+        dist.destroy_process_group()
