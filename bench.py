@@ -602,6 +602,18 @@ def secondary_configs(pifft, torch, gpu, steps, warmup, seed, cpu_threads, with_
     return out
 
 
+def _with_traffic(job, rf: dict, log_n: int, prec_bits: int) -> dict:
+    """rf with the PMC traffic of this rank's plan (load_traffic: the committed
+    profile of these very kernels, named by traffic_source), when one exists."""
+    key = f"n2^{log_n}_f{prec_bits}_b{job.batch_local}_P{job.P}_q{job.count}"
+    try:
+        rf["traffic"], rf["traffic_source"] = load_traffic(key, rf["launches"],
+                                                           [job.plan.kernel_name(i) for i in rf["launches"]])
+    except Exception as e:  # (optional: never costs the config its numbers)
+        rf["traffic"], rf["traffic_source"] = None, f"error: {e!r}"[:160]
+    return rf
+
+
 C5_HEADROOM = 4 << 30  # HBM left free beside config 5's largest phase
 
 
@@ -654,7 +666,8 @@ def config5(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, barrier, 
     job.time_launches(max(3, steps))
     rec.update({"value": round(5.0 * n * log_n / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s",
                 "ms_per_step": round(ms, 6), "steps": steps, "launches": job.launches(local_s * 1e3 / steps),
-                "roofline_rank0": job.roofline(local_s * 1e3 / steps) if rank == 0 else None})
+                "roofline_rank0": _with_traffic(job, job.roofline(local_s * 1e3 / steps), log_n, 64)
+                if rank == 0 else None})
 
     def _drop_replica():
         job.x = None  # the 64 GiB replica is not needed by the exchange
@@ -696,7 +709,8 @@ def multi_secondary(pifft, torch, dist, gpu, rank, world, steps, warmup, seed, b
             rec.update({"value": round(5.0 * (1 << log_n) * log_n * batch / (ms * 1e-3) / 1e9, 2),
                         "unit": "GFLOP/s", "ms_per_step": round(ms, 6), "steps": k, "n_gpus": world,
                         "dtype": "f64" if prec == F64 else "f32", "batch_per_gpu": g["batch_local"],
-                        "roofline_rank0": job.roofline(local_s * 1e3 / k) if rank == 0 else None})
+                        "roofline_rank0": _with_traffic(job, job.roofline(local_s * 1e3 / k), log_n,
+                                                        64 if prec == F64 else 32) if rank == 0 else None})
             if key == "C2_split":  # a worker split: check it (slices bitwise, gathered result vs one GPU)
                 exchange_and_verify(pifft, torch, dist, job, rank, world, barrier, red_dev, rec)
             job.free()
