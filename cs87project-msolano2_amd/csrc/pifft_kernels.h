@@ -758,29 +758,46 @@ __device__ __forceinline__ void pl_swap(cx<T>& a, cx<T>& b) {
     __builtin_memcpy(&b, y, sizeof b);
 }
 
-// Stage twiddles fetched with the data (PIFFT_TW_PREFETCH): the base anchor
-// w of every later stage's butterflies is loaded right after the tile's
-// inputs are issued, and w^2, w^4, w^8 are formed by squaring when the stage
-// runs -- instead of 2-4 table loads at the start of each stage, each a
+// Stage twiddles fetched with the data (PIFFT_TW_PREFETCH): the anchors of
+// every later stage's butterflies are loaded right after the tile's inputs
+// are issued (all of w, w^2, w^4, w^8, or only w with the others formed by
+// squaring when the stage runs) -- instead of 2-4 table loads at the start
+// of each stage, each a
 // dependent round trip on a workgroup's critical path.  That path is what
 // bounds the latency-bound small launches (one or two workgroups per CU);
 // the streaming passes hide it behind the other workgroup.
-// 0: off; 1: single passes (MODE 0/4) only; 2: every pass.  Measured on
-// MI355X (profiles/r02_ab_twiddle_prefetch.log): no gain on the small
-// launches (fp32 4096 x 512: 9 us either way; fp64 2^20: 24 us either way),
-// fp64 8192 x 64 single passes 11 -> 15 us (registers), C4 +3 % at 2 -- so off.
+// 0: off; 1: single passes (MODE 0/4) only; 2: every pass; 3: single and
+// first passes (MODE 0/1) of tiles built for at most 2 waves per SIMD (a
+// budget of 256 VGPRs), every anchor w, w^2, w^4, w^8 fetched from the table
+// (the values the stage would load itself: bitwise equal to 0; the 128-VGPR
+// instances would spill 4-46 VGPRs).
+// Measured on MI355X (profiles/r02_ab_twiddle_prefetch.log): no gain on the
+// small launches (fp32 4096 x 512: 9 us either way; fp64 2^20: 24 us either
+// way), fp64 8192 x 64 single passes 11 -> 15 us (registers), C4 +3 % at 2 --
+// so off; round 6 (profiles/r06s_*): at 2, config 3's single pass 47 -> 45
+// us and the first passes of C1 / C4 1-2 % faster, config 2's and C4's
+// later passes 3-11 % slower (spills at 128 VGPRs) -- hence 3, the default
+// since round 6 (profiles/r06t_*: outputs bitwise equal to 0 on 15 plans;
+// config 3 +1.4 %, config 1 +0.9 %, fp64 4096 x 1024 +5.5 %, fp64 2^22 +1.2 %,
+// configs 2 and 4 tie).
 #ifndef PIFFT_TW_PREFETCH
-#define PIFFT_TW_PREFETCH 0
+#define PIFFT_TW_PREFETCH 3
 #endif
 template <int R, int C, int BM, int VPT>
 constexpr bool tw_prefetch() {
-    return PIFFT_TW_PREFETCH == 2 || (PIFFT_TW_PREFETCH == 1 && BM == 0);
+    return PIFFT_TW_PREFETCH == 2 || (PIFFT_TW_PREFETCH == 1 && BM == 0) ||
+           (PIFFT_TW_PREFETCH == 3 && (BM == 0 || BM == 1) && PassCfg<R, C, VPT>::waves_per_eu <= 2);
 }
-// anchors of stages 1 .. S-1 (one per butterfly of a thread)
+// anchors fetched per butterfly of a radix-q stage: all log2 q (3), or the
+// base one, the others formed by squaring (1, 2)
+template <int q>
+constexpr int pre_anchors() { return PIFFT_TW_PREFETCH == 3 ? ilog2c(q) : 1; }
+// anchors of stages 1 .. S-1
 template <int R, int C, int BM, int VPT, int S>
 constexpr int pre_offset() {
     if constexpr (S <= 1) return 0;
-    else return pre_offset<R, C, BM, VPT, S - 1>() + Stage<R, C, BM, S - 1, VPT>::U;
+    else return pre_offset<R, C, BM, VPT, S - 1>() +
+                Stage<R, C, BM, S - 1, VPT>::U * pre_anchors<Stage<R, C, BM, S - 1, VPT>::q>();
 }
 template <int R, int C, int BM, int VPT>
 constexpr int pre_count() {
@@ -1070,7 +1087,10 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             for (int u = 0; u < St2::U; u++) {
                 int c, b;
                 St2::map(tid, u, c, b);
-                pre[pre_offset<R, C, SM, VPT, S2>() + u] = twr[(b & (St2::ns - 1)) * (R / (St2::ns * St2::q))];
+                constexpr int NA = pre_anchors<St2::q>();
+                const int e1 = (b & (St2::ns - 1)) * (R / (St2::ns * St2::q));
+#pragma unroll
+                for (int i = 0; i < NA; i++) pre[pre_offset<R, C, SM, VPT, S2>() + u * NA + i] = twr[e1 << i];
             }
         });
     }
@@ -1107,9 +1127,11 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             const int e1 = (b & (ns - 1)) * (R / (ns * q));
             C2 anc[4];
             if constexpr (tw_prefetch<R, C, BM, VPT>()) {
-                anc[0] = pre[pre_offset<R, C, SM, VPT, S>() + u];
+                constexpr int NA = pre_anchors<q>();
 #pragma unroll
-                for (int i = 1; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
+                for (int i = 0; i < NA; i++) anc[i] = pre[pre_offset<R, C, SM, VPT, S>() + u * NA + i];
+#pragma unroll
+                for (int i = NA; (1 << i) < q; i++) anc[i] = cmul(anc[i - 1], anc[i - 1]);
             } else {
 #pragma unroll
                 for (int i = 0; (1 << i) < q; i++) anc[i] = twr[e1 << i];

@@ -3,7 +3,9 @@
 libpifft (PIFFT_LIB) and write each output's SHA-256 to stdout; two runs with
 two builds, diffed, show whether a kernel change kept the results bit for bit
 (round 6: the one-round-trip tree twiddle fetch, tree_tw_fetch, against the
-round-5 kernels).  usage: PIFFT_LIB=abvar/x.so python3 tools/bitwise_libs.py"""
+round-5 kernels; the stage-twiddle prefetch, PIFFT_TW_PREFETCH=3, against
+HEAD's kernels on one-worker plans: --set single).
+usage: PIFFT_LIB=abvar/x.so python3 tools/bitwise_libs.py [--set tree|single]"""
 import hashlib
 import os
 import sys
@@ -16,6 +18,12 @@ import pifft  # noqa: E402
 
 SHAPES = [(20, 8, 1, 64), (19, 8, 1, 64), (20, 4, 1, 64), (18, 4, 1, 64), (22, 8, 1, 64), (20, 2, 1, 64),
           (20, 8, 1, 32), (18, 8, 1, 32), (21, 8, 1, 32), (12, 8, 64, 64), (17, 8, 16, 64), (24, 8, 1, 64)]
+# one-worker plans: single and first passes of every radix the planner picks at these sizes
+SINGLE = [(20, 1, 1, 64), (12, 1, 4096, 32), (12, 1, 64, 64), (10, 1, 512, 32), (11, 1, 256, 64), (13, 1, 64, 64),
+          (16, 1, 1, 64), (18, 1, 1, 64), (22, 1, 1, 64), (20, 1, 1, 32), (22, 1, 1, 32), (24, 1, 1, 32),
+          (9, 1, 1024, 64), (14, 1, 16, 32), (26, 1, 1, 64)]
+if "--set" in sys.argv and sys.argv[sys.argv.index("--set") + 1] == "single":
+    SHAPES = SINGLE
 
 for logn, P, batch, prec in SHAPES:
     n = 1 << logn
