@@ -780,6 +780,9 @@ __device__ __forceinline__ void pl_swap(cx<T>& a, cx<T>& b) {
 // since round 6 (profiles/r06t_*: outputs bitwise equal to 0 on 15 plans;
 // config 3 +1.4 %, config 1 +0.9 %, fp64 4096 x 1024 +5.5 %, fp64 2^22 +1.2 %,
 // configs 2 and 4 tie).
+#ifndef PIFFT_DIAG_NO_XCHG
+#define PIFFT_DIAG_NO_XCHG 0  // diagnostics: skip the LDS hand-offs between stages (timing only)
+#endif
 #ifndef PIFFT_TW_PREFETCH
 #define PIFFT_TW_PREFETCH 3
 #endif
@@ -1216,6 +1219,11 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 #pragma unroll
             for (int g = 0; g < 8; g++) pl_swap<16>(v[2 * g], v[2 * g + 1]);
         }
+        pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile, twp);
+    } else if constexpr (PIFFT_DIAG_NO_XCHG && MODE != 11) {
+        // diagnostics build only (timing, WRONG results): no hand-off at all --
+        // the upper bound of what any register exchange (DPP, ds_swizzle,
+        // permlane) could save on this pass (round 6, tools/gpu_r06w.sh)
         pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile, twp);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
