@@ -1223,7 +1223,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
     } else if constexpr (PIFFT_DIAG_NO_XCHG && MODE != 11) {
         // diagnostics build only (timing, WRONG results): no hand-off at all --
         // the upper bound of what any register exchange (DPP, ds_swizzle,
-        // permlane) could save on this pass (round 6, tools/gpu_r06w.sh)
+        // permlane) could save on this pass (round 6, profiles/sessions/gpu_r06w.sh)
         pass_stages<T, R, C, MODE, NTS, LP, S + 1, VPT>(a, lds, v, pre, tid, tile, twp);
     } else {
         // ---- exchange with stage S+1 through LDS, one component at a time ----
@@ -1275,7 +1275,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
 // packed fp32 passes without their twiddles (PIFFT_DIAG_NO_TW=1: no table
 // loads, no twiddle products) or without their butterflies
 // (PIFFT_DIAG_NO_DFT=1), to split a pass's time between its data movement,
-// LDS exchanges, twiddles and arithmetic (round 6, tools/gpu_r06g.sh).
+// LDS exchanges, twiddles and arithmetic (round 6, profiles/sessions/gpu_r06g.sh).
 #ifndef PIFFT_DIAG_NO_TW
 #define PIFFT_DIAG_NO_TW 0
 #endif
