@@ -1031,12 +1031,14 @@ int build_plan(pifft_plan* p, bool dry = false) {
         const bool fuse_here = (i == 0 && fused);
         const bool last_pass = i + 1 == passes.size() && passes.size() > 1;
         // tuning: the last pass's streaming form (0 plain, 1 nt both, 2 nt loads, 3 nt stores)
-        int last_nt = last_pass && passes[i].mode == 2 ? env_int("PIFFT_LAST_NT", -1) : -1;
-        // (and the first pass's, 0 plain / 1 nt both, of a plan without a fused tree)
-        if (i == 0 && !fuse_here && passes.size() > 1 && passes[i].mode == 1) last_nt = env_int("PIFFT_FIRST_NT", -1);
+        int nt_override = last_pass && passes[i].mode == 2 ? env_int("PIFFT_LAST_NT", -1) : -1;
+        // (and the first pass's, 0 plain / 1 nt both, of a plan without a fused tree; round 6,
+        // profiles/r06y3_*: the default stays)
+        if (i == 0 && !fuse_here && passes.size() > 1 && passes[i].mode == 1)
+            nt_override = env_int("PIFFT_FIRST_NT", -1);
         const PassKernel* k = fuse_here ? fused
                                         : find_pass(p->prec, passes[i].R, passes[i].C, passes[i].mode,
-                                                    last_nt >= 0 ? last_nt : passes[i].nts, 0, passes[i].vpt);
+                                                    nt_override >= 0 ? nt_override : passes[i].nts, 0, passes[i].vpt);
         if (!k) return fail("no pass kernel R=%d C=%d", passes[i].R, passes[i].C);
         Step s;
         s.kind = fuse_here ? STEP_TREE_PASS : STEP_PASS;
