@@ -817,6 +817,17 @@ constexpr int pass_waves_per_eu() {
     constexpr int w = PassCfg<R, C, VPT>::waves_per_eu;
     return ((MODE & 3) == 3 && LP >= 5) ? 1 : ((MODE & 3) == 3 && LP >= 4 && w > 2) ? 2 : w;
 }
+// The stage-twiddle prefetch of a k_pass instance: tw_prefetch, and (at 3)
+// the one-worker fused tree pass (MODE 3) of 256-VGPR tiles as well -- round 6
+// (profiles/r06y5_*): config 2's one-GPU slice +1.9 %, bitwise equal; the
+// all-worker fused pass (MODE 11) measured 0.3 % slower with it, so not there.
+template <typename T, int R, int C, int MODE, int LP, int VPT>
+constexpr bool pass_tw_prefetch() {
+    if constexpr (PIFFT_TW_PREFETCH == 3 && (MODE & 3) == 3 && !(MODE & 8) &&
+                  pass_waves_per_eu<T, R, C, MODE, LP, VPT>() <= 2)
+        return true;
+    return tw_prefetch<R, C, MODE & 3, VPT>();
+}
 
 // MODE 11 = 3 | 8: the tree of ALL P = 2^LP workers fused into the first
 // worker-interleaved pass (an all-worker natural-order plan, PassArgs::wil =
@@ -1081,7 +1092,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
         }
     }
     if constexpr (St::first) PIFFT_WGC(3);
-    if constexpr (St::first && tw_prefetch<R, C, BM, VPT>()) {
+    if constexpr (St::first && pass_tw_prefetch<T, R, C, MODE, LP, VPT>()) {
         const C2* __restrict__ twr = static_cast<const C2*>(a.tw_r);
         static_for<1, Sh::NSTG, 1>([&](auto sc) {
             constexpr int S2 = decltype(sc)::value;
@@ -1129,7 +1140,7 @@ __device__ __forceinline__ void pass_stages(const PassArgs& a, T* lds, cx<T>* v,
             St::map(tid, u, c, b);
             const int e1 = (b & (ns - 1)) * (R / (ns * q));
             C2 anc[4];
-            if constexpr (tw_prefetch<R, C, BM, VPT>()) {
+            if constexpr (pass_tw_prefetch<T, R, C, MODE, LP, VPT>()) {
                 constexpr int NA = pre_anchors<q>();
 #pragma unroll
                 for (int i = 0; i < NA; i++) anc[i] = pre[pre_offset<R, C, SM, VPT, S>() + u * NA + i];
